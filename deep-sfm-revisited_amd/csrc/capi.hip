@@ -1,0 +1,111 @@
+// Error reporting and per-kernel event profiling for libsfm_hip.
+#include <mutex>
+#include <vector>
+#include <cstring>
+#include "common.h"
+
+namespace sfm {
+
+static thread_local std::string g_error;
+
+void set_error(const std::string& msg) { g_error = msg; }
+
+namespace {
+struct Slot {
+  std::string name;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  double total_ms = 0.0;
+  int launches = 0;
+};
+std::mutex g_mu;
+bool g_enabled = false;
+std::vector<Slot> g_slots;
+std::vector<hipEvent_t> g_pool;
+
+hipEvent_t take_event() {
+  if (!g_pool.empty()) { hipEvent_t e = g_pool.back(); g_pool.pop_back(); return e; }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+int slot_of(const char* name) {
+  for (size_t i = 0; i < g_slots.size(); ++i)
+    if (g_slots[i].name == name) return (int)i;
+  g_slots.push_back(Slot{name, {}, 0.0, 0});
+  return (int)g_slots.size() - 1;
+}
+
+// Fold completed event pairs of a slot into its totals (blocks on them).
+void drain(Slot& s) {
+  for (auto& ev : s.events) {
+    (void)hipEventSynchronize(ev.second);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ev.first, ev.second) == hipSuccess) {
+      s.total_ms += ms;
+      s.launches += 1;
+    }
+    g_pool.push_back(ev.first);
+    g_pool.push_back(ev.second);
+  }
+  s.events.clear();
+}
+}  // namespace
+
+ProfScope::ProfScope(const char* name, hipStream_t s) : slot(-1), stream(s) {
+  if (!g_enabled) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  slot = slot_of(name);
+  hipEvent_t a = take_event(), b = take_event();
+  if (!a || !b) { slot = -1; return; }
+  (void)hipEventRecord(a, stream);
+  g_slots[slot].events.emplace_back(a, b);
+}
+
+ProfScope::~ProfScope() {
+  if (slot < 0) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  (void)hipEventRecord(g_slots[slot].events.back().second, stream);
+  if (g_slots[slot].events.size() > 256) drain(g_slots[slot]);
+}
+
+}  // namespace sfm
+
+extern "C" {
+
+int sfm_abi_version(void) { return SFM_ABI_VERSION; }
+
+const char* sfm_last_error(void) { return sfm::g_error.c_str(); }
+
+int sfm_profile_enable(int on) {
+  std::lock_guard<std::mutex> lk(sfm::g_mu);
+  sfm::g_enabled = on != 0;
+  return SFM_OK;
+}
+
+int sfm_profile_reset(void) {
+  std::lock_guard<std::mutex> lk(sfm::g_mu);
+  for (auto& s : sfm::g_slots) {
+    sfm::drain(s);
+    s.total_ms = 0.0;
+    s.launches = 0;
+  }
+  return SFM_OK;
+}
+
+int sfm_profile_read(const char* name, double* total_ms, int* launches) {
+  if (!name || !total_ms || !launches) { sfm::set_error("sfm_profile_read: null argument"); return SFM_ERR_ARG; }
+  std::lock_guard<std::mutex> lk(sfm::g_mu);
+  for (auto& s : sfm::g_slots)
+    if (s.name == name) {
+      sfm::drain(s);
+      *total_ms = s.total_ms;
+      *launches = s.launches;
+      return SFM_OK;
+    }
+  *total_ms = 0.0;
+  *launches = 0;
+  return SFM_OK;
+}
+
+}  // extern "C"

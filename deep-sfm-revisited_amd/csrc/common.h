@@ -1,0 +1,46 @@
+// Internal helpers shared by the libsfm_hip translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include "sfm_hip.h"
+
+namespace sfm {
+
+void set_error(const std::string& msg);
+
+// Profiling hooks (capi.hip): record HIP events around a launch when enabled.
+struct ProfScope {
+  ProfScope(const char* name, hipStream_t s);
+  ~ProfScope();
+  int slot;
+  hipStream_t stream;
+};
+
+}  // namespace sfm
+
+#define SFM_REQUIRE(cond, msg)                 \
+  do {                                         \
+    if (!(cond)) {                             \
+      ::sfm::set_error(msg);                   \
+      return SFM_ERR_ARG;                      \
+    }                                          \
+  } while (0)
+
+#define SFM_HIP(call)                                                             \
+  do {                                                                            \
+    hipError_t e_ = (call);                                                       \
+    if (e_ != hipSuccess) {                                                       \
+      ::sfm::set_error(std::string(#call) + ": " + hipGetErrorString(e_));        \
+      return SFM_ERR_HIP;                                                         \
+    }                                                                             \
+  } while (0)
+
+#define SFM_LAUNCHED()                                                            \
+  do {                                                                            \
+    hipError_t e_ = hipGetLastError();                                            \
+    if (e_ != hipSuccess) {                                                       \
+      ::sfm::set_error(std::string("kernel launch: ") + hipGetErrorString(e_));   \
+      return SFM_ERR_HIP;                                                         \
+    }                                                                             \
+  } while (0)

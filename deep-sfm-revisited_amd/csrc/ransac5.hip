@@ -1,0 +1,648 @@
+// RANSAC five-point essential matrix on CDNA4 (gfx950).
+//
+// Replaces the reference's essential_matrix extension hot path
+// (RANSAC_FiveP/essential_matrix/essential_matrix.cu:110-280 host drivers,
+// kernel_functions.cu:53-226 kernels).  The reference runs 512 threads, each
+// looping over `ransac_iter` hypotheses and scoring every candidate E against
+// all N correspondences serially.  Here the same semantics are split into
+// data-parallel phases:
+//
+//   k_solve   one lane per hypothesis: Philox sample, five-point solve,
+//             cheirality, compaction.                      (latency-bound)
+//   k_chain   one lane per reference thread ("chain"): resolves the stale
+//             slot-0 E/P state a chain carries across its iterations and
+//             emits a dense candidate list (prefix sum per pair).
+//   k_score   persistent, tiles of 32 candidates x 8192 points: the
+//             Sampson-style inlier test, wave-ballot popcounts, int atomics.
+//                                                           (fp64-VALU-bound)
+//   k_select  per pair: preselect/rescore per hypothesis, first-max argmax.
+//
+// Inlier decisions are bit-identical to the reference's IEEE evaluation
+// |x'^T E x| / sqrt(Ex0^2+Ex1^2+xE0^2+xE1^2) <= thr: the products and sums are
+// evaluated in the reference's order without contraction, and the
+// sqrt+division is replaced by a squared comparison with a 2^-40 relative
+// guard band; the (rare) values inside the band take the exact IEEE path.
+#include <algorithm>
+#include <vector>
+#include "common.h"
+#include "five_point.h"
+
+namespace sfm {
+
+constexpr int kChains = SFM_RANSAC_CHAINS;
+constexpr int kMaxSlots = 10;
+constexpr int kCandStride = 12;   // doubles per candidate E (9 used), 96 B
+constexpr int kKC = 32;           // candidates per score tile
+constexpr int kPPL = 4;           // points per lane per chunk
+constexpr int kScoreThreads = 256;
+constexpr int kChunk = kScoreThreads * kPPL;
+constexpr int kChunksPerItem = 8;
+constexpr int kPtsPerItem = kChunk * kChunksPerItem;   // 8192
+constexpr double kDmin = 0x1p-900;
+
+struct PairParams {
+  int64_t n[SFM_MAX_BATCH];
+  int32_t test[SFM_MAX_BATCH];     // num_test_points
+  int32_t rtest[SFM_MAX_BATCH];    // num_ransac_test_points
+  int32_t splits[SFM_MAX_BATCH];   // point splits of max(test, rtest)
+};
+
+struct Workspace {
+  int32_t* nroots;     // [B][H]
+  int32_t* ncand;      // [B][H]
+  double* hypE;        // [B][H][10][9]
+  double* hypP;        // [B][H][10][12]
+  double* hypP0;       // [B][H][12]
+  int32_t* cand_off;   // [B][H]
+  int32_t* cand_total; // [64]
+  double* candE;       // [B][Cmax][12]
+  int32_t* cntT;       // [B][Cmax]
+  int32_t* cntR;       // [B][Cmax]
+  int32_t* score;      // [B][H]
+  double* pack;        // [n_max][4]
+};
+
+static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// Lay out the workspace; returns the byte count (ptrs filled when base != nullptr).
+static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w) {
+  const size_t H = (size_t)kChains * iters, C = H * kMaxSlots;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* p = base ? base + off : nullptr; off += align_up(bytes); return p; };
+  Workspace t;
+  t.nroots = (int32_t*)take(bc * H * 4);
+  t.ncand = (int32_t*)take(bc * H * 4);
+  t.hypE = (double*)take(bc * H * kMaxSlots * 9 * 8);
+  t.hypP = (double*)take(bc * H * kMaxSlots * 12 * 8);
+  t.hypP0 = (double*)take(bc * H * 12 * 8);
+  t.cand_off = (int32_t*)take(bc * H * 4);
+  t.cand_total = (int32_t*)take(SFM_MAX_BATCH * 4);
+  t.candE = (double*)take(bc * C * kCandStride * 8);
+  t.cntT = (int32_t*)take(bc * C * 4);
+  t.cntR = (int32_t*)take(bc * C * 4);
+  t.score = (int32_t*)take(bc * H * 4);
+  t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
+  if (w) *w = t;
+  return off;
+}
+
+// ---------------------------------------------------------------------------
+// Phase 1: one lane per hypothesis
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, int64_t n_stride,
+                                              PairParams pp, int H, uint64_t seed, int cheir,
+                                              int32_t* __restrict__ out_nroots, int32_t* __restrict__ out_ncand,
+                                              double* __restrict__ hypE, double* __restrict__ hypP) {
+  const int b = blockIdx.y;
+  const int h = blockIdx.x * 64 + threadIdx.x;
+  if (h >= H) return;
+  const int64_t n = pp.n[b];
+  int64_t idx[5];
+  sample5(seed, (uint32_t)h, n, idx);
+  const double* P = pts + (size_t)b * n_stride * 4;
+  double q[5][2], qp[5][2];
+#pragma unroll
+  for (int d = 0; d < 5; ++d) {
+    const double4 v = *reinterpret_cast<const double4*>(P + idx[d] * 4);
+    q[d][0] = v.x; q[d][1] = v.y; qp[d][0] = v.z; qp[d][1] = v.w;
+  }
+  Lin Eb[9];
+  essential_basis(q, qp, Eb);
+  Eqs A;
+  build_equations(Eb, A);
+  reduce_equations(A);
+  double poly[11];
+  determinant_poly(A, poly);
+  double roots[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) roots[i] = 0.0;
+  const int nr = real_roots(poly, roots);
+  const int nv = nr > 0 ? (nr < 10 ? nr : 10) : 0;
+  const size_t hb = (size_t)b * H + h;
+  double* Eo = hypE + hb * kMaxSlots * 9;
+  double* Po = hypP + hb * kMaxSlots * 12;
+  int nc = 0;
+  for (int m = 0; m < nv; ++m) {
+    double E[9];
+    essential_at_root(Eb, A, roots[m], E);
+    if (!cheir) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) Eo[m * 9 + e] = E[e];
+      ++nc;
+      continue;
+    }
+    double Pm[12];
+    const bool ok = cheirality_P(E, q, qp, Pm);
+    // compaction (cheirality.cu:142-146): accepted E's move to the front; if
+    // none is accepted slot 0 keeps root 0's E.
+    if (ok) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) Eo[nc * 9 + e] = E[e];
+#pragma unroll
+      for (int e = 0; e < 12; ++e) Po[nc * 12 + e] = Pm[e];
+      ++nc;
+    } else if (m == 0) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) Eo[e] = E[e];
+    }
+  }
+  out_nroots[hb] = nr;
+  out_ncand[hb] = nc;
+}
+
+// ---------------------------------------------------------------------------
+// Phase 2: chains and the dense candidate list (one block of 512 per pair)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
+                                                   const int32_t* __restrict__ nroots,
+                                                   const int32_t* __restrict__ ncand,
+                                                   const double* __restrict__ hypE,
+                                                   const double* __restrict__ hypP,
+                                                   double* __restrict__ hypP0,
+                                                   int32_t* __restrict__ cand_off,
+                                                   int32_t* __restrict__ cand_total,
+                                                   double* __restrict__ candE, int cmax) {
+  __shared__ int32_t s_sum[kChains / 64];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const size_t hb0 = (size_t)b * H;
+  int cnt = 0;
+  for (int i = 0; i < iters; ++i) {
+    const int nc = ncand[hb0 + t * iters + i];
+    cnt += nc > 0 ? nc : 1;
+  }
+  // block exclusive scan over chains
+  const int lane = t & 63, wv = t >> 6;
+  int incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) s_sum[wv] = incl;
+  __syncthreads();
+  int base = incl - cnt;
+  for (int w = 0; w < wv; ++w) base += s_sum[w];
+  if (t == kChains - 1) cand_total[b] = base + cnt;
+
+  double E0[9], P0[12];
+#pragma unroll
+  for (int e = 0; e < 9; ++e) E0[e] = 0.0;
+#pragma unroll
+  for (int e = 0; e < 12; ++e) P0[e] = 0.0;
+  int off = base;
+  double* cE = candE + (size_t)b * cmax * kCandStride;
+  for (int i = 0; i < iters; ++i) {
+    const int h = t * iters + i;
+    const size_t hb = hb0 + h;
+    const int nr = nroots[hb], nc = ncand[hb];
+    const double* Eh = hypE + hb * kMaxSlots * 9;
+    cand_off[hb] = off;
+    if (nc > 0) {
+      for (int j = 0; j < nc; ++j)
+#pragma unroll
+        for (int e = 0; e < 9; ++e) cE[(size_t)(off + j) * kCandStride + e] = Eh[j * 9 + e];
+      off += nc;
+    } else {
+      // rescore-only candidate: slot 0 as the reference thread would hold it
+#pragma unroll
+      for (int e = 0; e < 9; ++e) cE[(size_t)off * kCandStride + e] = nr > 0 ? Eh[e] : E0[e];
+#pragma unroll
+      for (int e = 0; e < 12; ++e) hypP0[hb * 12 + e] = P0[e];
+      off += 1;
+    }
+    if (nr > 0) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) E0[e] = Eh[e];
+    }
+    if (cheir && nc > 0) {
+      const double* Ph = hypP + hb * kMaxSlots * 12;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) P0[e] = Ph[e];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase 3: scoring
+// ---------------------------------------------------------------------------
+struct ScoreConsts {
+  double thr, t2lo, t2hi;
+};
+
+// Exact reference evaluation (ComputeError, kernel_functions.cu:232-264).
+__device__ __forceinline__ bool inlier_exact(double a, double D, double thr) {
+  double e = a / sqrt(D);
+  if (e < 0.0) e = -e;
+  return e <= thr;
+}
+
+template <bool FAST>
+__device__ __forceinline__ bool inlier_test(const double* E, double x, double y, double xp, double yp,
+                                            const ScoreConsts& k) {
+  const double ex0 = (E[0] * x + E[1] * y) + E[2];
+  const double ex1 = (E[3] * x + E[4] * y) + E[5];
+  const double ex2 = (E[6] * x + E[7] * y) + E[8];
+  const double xe0 = (xp * E[0] + yp * E[3]) + E[6];
+  const double xe1 = (xp * E[1] + yp * E[4]) + E[7];
+  const double a = (xp * ex0 + yp * ex1) + ex2;
+  const double D = ((ex0 * ex0 + ex1 * ex1) + xe0 * xe0) + xe1 * xe1;
+  if (!FAST) return inlier_exact(a, D, k.thr);
+  const double lhs = a * a;
+  const bool g = D >= kDmin;
+  const bool fin = g && (lhs < k.t2lo * D);
+  const bool fout = g && (lhs > k.t2hi * D);
+  bool in = fin;
+  if (!(fin || fout)) in = inlier_exact(a, D, k.thr);
+  return in;
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restrict__ pts, int64_t n_stride,
+                                                         PairParams pp, int batch, int cmax,
+                                                         const int32_t* __restrict__ cand_total,
+                                                         const double* __restrict__ candE,
+                                                         int32_t* __restrict__ cntT, int32_t* __restrict__ cntR,
+                                                         ScoreConsts kc) {
+  __shared__ int32_t s_cnt[kScoreThreads / 64][kKC][2];
+  __shared__ int32_t s_items[SFM_MAX_BATCH + 1];
+  __shared__ int32_t s_tiles[SFM_MAX_BATCH];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) {
+    int acc = 0;
+    for (int b = 0; b < batch; ++b) {
+      const int tiles = (cand_total[b] + kKC - 1) / kKC;
+      s_tiles[b] = tiles;
+      s_items[b] = acc;
+      acc += tiles * pp.splits[b];
+    }
+    s_items[batch] = acc;
+  }
+  for (int i = tid; i < (kScoreThreads / 64) * kKC * 2; i += kScoreThreads) (&s_cnt[0][0][0])[i] = 0;
+  __syncthreads();
+  const int total = s_items[batch];
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    int b = 0;
+    while (item >= s_items[b + 1]) ++b;
+    const int local = item - s_items[b];
+    const int tiles = s_tiles[b];
+    const int split = local / tiles, tile = local - split * tiles;
+    const int ctot = cand_total[b];
+    const int c0 = tile * kKC;
+    const int nc = min(kKC, ctot - c0);
+    const int T = pp.test[b], R = pp.rtest[b];
+    const int M = max(T, R);
+    const int p0 = split * kPtsPerItem;
+    const int p1 = min(M, p0 + kPtsPerItem);
+    const double* P = pts + (size_t)b * n_stride * 4;
+    const double* CE = candE + ((size_t)b * cmax + c0) * kCandStride;
+    for (int cb = p0; cb < p1; cb += kChunk) {
+      double x[kPPL], y[kPPL], xp[kPPL], yp[kPPL];
+      bool vT[kPPL], vR[kPPL];
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) {
+        const int p = cb + k * kScoreThreads + tid;
+        const bool ok = p < p1;
+        const double4 v = *reinterpret_cast<const double4*>(P + (size_t)(ok ? p : p0) * 4);
+        x[k] = v.x; y[k] = v.y; xp[k] = v.z; yp[k] = v.w;
+        vT[k] = ok && p < T;
+        vR[k] = ok && p < R;
+      }
+      for (int c = 0; c < nc; ++c) {
+        double E[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) E[e] = CE[(size_t)c * kCandStride + e];
+        int sT = 0, sR = 0;
+#pragma unroll
+        for (int k = 0; k < kPPL; ++k) {
+          const bool in = inlier_test<FAST>(E, x[k], y[k], xp[k], yp[k], kc);
+          sT += __popcll(__ballot(in && vT[k]));
+          sR += __popcll(__ballot(in && vR[k]));
+        }
+        if (lane == 0) {
+          s_cnt[wv][c][0] += sT;
+          s_cnt[wv][c][1] += sR;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < nc * 2) {
+      const int c = tid >> 1, which = tid & 1;
+      int s = 0;
+#pragma unroll
+      for (int w = 0; w < kScoreThreads / 64; ++w) { s += s_cnt[w][c][which]; s_cnt[w][c][which] = 0; }
+      if (s) atomicAdd((which ? cntR : cntT) + (size_t)b * cmax + c0 + c, s);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase 4: selection (one block per pair)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_select(int H, int cmax, int cheir,
+                                                 const int32_t* __restrict__ ncand,
+                                                 const int32_t* __restrict__ cand_off,
+                                                 const int32_t* __restrict__ cntT,
+                                                 const int32_t* __restrict__ cntR,
+                                                 const double* __restrict__ candE,
+                                                 const double* __restrict__ hypP,
+                                                 const double* __restrict__ hypP0,
+                                                 int32_t* __restrict__ score_out,
+                                                 double* __restrict__ E_out, double* __restrict__ P_out,
+                                                 int32_t* __restrict__ inliers_out, int32_t* __restrict__ winner_out) {
+  __shared__ unsigned long long s_best[16];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const size_t hb0 = (size_t)b * H;
+  const int32_t* cT = cntT + (size_t)b * cmax;
+  const int32_t* cR = cntR + (size_t)b * cmax;
+  unsigned long long best = 0ull;
+  for (int h = tid; h < H; h += blockDim.x) {
+    const int nc = ncand[hb0 + h], off = cand_off[hb0 + h];
+    int bi = 0, bc = 0;
+    for (int j = 0; j < nc; ++j) {
+      const int c = cT[off + j];
+      if (c > bc) { bc = c; bi = j; }
+    }
+    const int s = cR[off + bi];
+    score_out[hb0 + h] = s;
+    const unsigned long long key = ((unsigned long long)(uint32_t)s << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)h);
+    best = key > best ? key : best;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const unsigned long long o = __shfl_xor(best, d, 64);
+    best = o > best ? o : best;
+  }
+  if ((tid & 63) == 0) s_best[tid >> 6] = best;
+  __syncthreads();
+  if (tid != 0) return;
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = s_best[w] > best ? s_best[w] : best;
+  const int s = (int)(best >> 32);
+  double* Eo = E_out + (size_t)b * 9;
+  double* Po = P_out ? P_out + (size_t)b * 12 : nullptr;
+  if (s <= 0) {
+    for (int e = 0; e < 9; ++e) Eo[e] = 0.0;
+    if (Po) for (int e = 0; e < 12; ++e) Po[e] = 0.0;
+    inliers_out[b] = 0;
+    if (winner_out) winner_out[b] = -1;
+    return;
+  }
+  const int h = (int)(0xFFFFFFFFu - (uint32_t)(best & 0xFFFFFFFFull));
+  const int nc = ncand[hb0 + h], off = cand_off[hb0 + h];
+  int bi = 0, bc = 0;
+  for (int j = 0; j < nc; ++j) {
+    const int c = cT[off + j];
+    if (c > bc) { bc = c; bi = j; }
+  }
+  const double* Ew = candE + ((size_t)b * cmax + off + bi) * kCandStride;
+  for (int e = 0; e < 9; ++e) Eo[e] = Ew[e];
+  if (Po) {
+    const double* Pw = nc > 0 ? hypP + ((hb0 + h) * kMaxSlots + bi) * 12 : hypP0 + (hb0 + h) * 12;
+    for (int e = 0; e < 12; ++e) Po[e] = cheir ? Pw[e] : 0.0;
+  }
+  inliers_out[b] = s;
+  if (winner_out) winner_out[b] = h;
+}
+
+// ---------------------------------------------------------------------------
+// Auxiliary kernels
+// ---------------------------------------------------------------------------
+__global__ void k_inlier_mask(const double* __restrict__ pts, int64_t n_stride, PairParams pp,
+                              const double* __restrict__ E, double thr, uint8_t* __restrict__ mask) {
+  const int b = blockIdx.y;
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_stride) return;
+  uint8_t m = 0;
+  if (k < pp.n[b]) {
+    const double4 v = *reinterpret_cast<const double4*>(pts + ((size_t)b * n_stride + k) * 4);
+    const ScoreConsts kc{thr, 0.0, 0.0};
+    m = inlier_test<false>(E + (size_t)b * 9, v.x, v.y, v.z, v.w, kc) ? 1 : 0;
+  }
+  mask[(size_t)b * n_stride + k] = m;
+}
+
+__global__ void k_pack(const double* __restrict__ q, const double* __restrict__ qp, int64_t n, double* __restrict__ out) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double2 a = reinterpret_cast<const double2*>(q)[k];
+  const double2 c = reinterpret_cast<const double2*>(qp)[k];
+  reinterpret_cast<double4*>(out)[k] = make_double4(a.x, a.y, c.x, c.y);
+}
+
+// flow2coord + margin crop + K^-1 (models/SFMnet.py:179-263, 298-318)
+__global__ void k_flow_points(const float* __restrict__ flow, int H, int W, int h_side, int w_side, int margin,
+                              const float* __restrict__ Kinv, double* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int wn = w_side - 2 * margin, hn = h_side - 2 * margin;
+  const int64_t N = (int64_t)wn * hn;
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N) return;
+  const int v = (int)(k / wn) + margin, u = (int)(k % wn) + margin;
+  const float* Ki = Kinv + b * 9;
+  const float* F = flow + (size_t)b * 2 * H * W;
+  const float fu = F[(size_t)v * W + u], fv = F[(size_t)H * W + (size_t)v * W + u];
+  const float u1 = (float)u, v1 = (float)v;
+  const float u2 = u1 + fu, v2 = v1 + fv;
+  const float x1 = (Ki[0] * u1 + Ki[1] * v1) + Ki[2];
+  const float y1 = (Ki[3] * u1 + Ki[4] * v1) + Ki[5];
+  const float x2 = (Ki[0] * u2 + Ki[1] * v2) + Ki[2];
+  const float y2 = (Ki[3] * u2 + Ki[4] * v2) + Ki[5];
+  reinterpret_cast<double4*>(out)[(size_t)b * N + k] = make_double4(x1, y1, x2, y2);
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------
+static int run_chunk(const double* pts, int64_t n_stride, const int64_t* n, int bc, int num_test,
+                     int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
+                     const Workspace& w, double* E_out, double* P_out, int32_t* inliers_out,
+                     int32_t* winner_out, int32_t* score_out, hipStream_t s) {
+  const int H = kChains * iters;
+  const int cmax = H * kMaxSlots;
+  PairParams pp{};
+  for (int b = 0; b < bc; ++b) {
+    pp.n[b] = n[b];
+    pp.test[b] = (int32_t)(num_test > 0 ? num_test : n[b]);
+    pp.rtest[b] = (int32_t)(num_ransac_test > 0 ? num_ransac_test : n[b]);
+    const int M = std::max(pp.test[b], pp.rtest[b]);
+    pp.splits[b] = (M + kPtsPerItem - 1) / kPtsPerItem;
+  }
+  {
+    ProfScope ps("ransac_solve", s);
+    hipLaunchKernelGGL(k_solve, dim3((H + 63) / 64, bc), dim3(64), 0, s, pts, n_stride, pp, H, seed, cheir,
+                       w.nroots, w.ncand, w.hypE, w.hypP);
+  }
+  SFM_LAUNCHED();
+  {
+    ProfScope ps("ransac_chain", s);
+    hipLaunchKernelGGL(k_chain, dim3(bc), dim3(kChains), 0, s, H, iters, cheir, w.nroots, w.ncand, w.hypE,
+                       w.hypP, w.hypP0, w.cand_off, w.cand_total, w.candE, cmax);
+  }
+  SFM_LAUNCHED();
+  SFM_HIP(hipMemsetAsync(w.cntT, 0, (size_t)bc * cmax * 4, s));
+  SFM_HIP(hipMemsetAsync(w.cntR, 0, (size_t)bc * cmax * 4, s));
+  const bool fast = thr >= 0x1p-40 && thr < 1.0;
+  ScoreConsts kc{thr, (thr * thr) * (1.0 - 0x1p-40), (thr * thr) * (1.0 + 0x1p-40)};
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = std::max(1, cus) * 8;
+  {
+    ProfScope ps("ransac_score", s);
+    if (fast)
+      hipLaunchKernelGGL(k_score<true>, dim3(grid), dim3(kScoreThreads), 0, s, pts, n_stride, pp, bc, cmax,
+                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
+    else
+      hipLaunchKernelGGL(k_score<false>, dim3(grid), dim3(kScoreThreads), 0, s, pts, n_stride, pp, bc, cmax,
+                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
+  }
+  SFM_LAUNCHED();
+  {
+    ProfScope ps("ransac_select", s);
+    hipLaunchKernelGGL(k_select, dim3(bc), dim3(1024), 0, s, H, cmax, cheir, w.ncand, w.cand_off, w.cntT,
+                       w.cntR, w.candE, w.hypP, w.hypP0, score_out ? score_out : w.score, E_out, P_out,
+                       inliers_out, winner_out);
+  }
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+static int check_common(int iters, double thr, int batch) {
+  SFM_REQUIRE(batch >= 1, "batch must be >= 1");
+  SFM_REQUIRE(iters >= 1 && iters <= 4096, "iters must be in [1, 4096]");
+  SFM_REQUIRE(thr > 0.0, "inlier threshold must be > 0");
+  return SFM_OK;
+}
+
+static int run_packed(const double* pts, int64_t n_stride, const int64_t* n, int batch, int num_test,
+                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir, void* ws,
+                      size_t ws_bytes, double* E_out, double* P_out, int32_t* inliers_out, int32_t* winner_out,
+                      int32_t* score_out, hipStream_t s) {
+  if (int rc = check_common(iters, thr, batch)) return rc;
+  SFM_REQUIRE(pts && n && E_out && inliers_out, "null pointer argument");
+  SFM_REQUIRE(cheir == 0 || P_out, "P_out required when cheirality is on");
+  SFM_REQUIRE(n_stride >= 1 && n_stride <= (int64_t)INT32_MAX, "n_stride out of range");
+  for (int b = 0; b < batch; ++b) {
+    SFM_REQUIRE(n[b] >= 1 && n[b] <= n_stride, "each n[b] must be in [1, n_stride]");
+    SFM_REQUIRE(num_test <= n[b] && num_ransac_test <= n[b],
+                "num_test_points / num_ransac_test_points must not exceed the number of points");
+  }
+  const int bc = std::min(batch, SFM_MAX_BATCH);
+  const size_t need = layout(nullptr, bc, 0, iters, nullptr);
+  if (!ws || ws_bytes < need) {
+    set_error("workspace too small: need " + std::to_string(need) + " bytes");
+    return SFM_ERR_WORKSPACE;
+  }
+  Workspace w;
+  layout((char*)ws, bc, 0, iters, &w);
+  const int H = kChains * iters;
+  for (int b0 = 0; b0 < batch; b0 += bc) {
+    const int nb = std::min(bc, batch - b0);
+    if (int rc = run_chunk(pts + (size_t)b0 * n_stride * 4, n_stride, n + b0, nb, num_test, num_ransac_test,
+                           iters, thr, seed, cheir, w, E_out + (size_t)b0 * 9, P_out ? P_out + (size_t)b0 * 12 : nullptr,
+                           inliers_out + b0, winner_out ? winner_out + b0 : nullptr,
+                           score_out ? score_out + (size_t)b0 * H : nullptr, s))
+      return rc;
+  }
+  return SFM_OK;
+}
+
+}  // namespace sfm
+
+using namespace sfm;
+
+extern "C" {
+
+size_t sfm_ransac5_workspace_bytes(int batch, int64_t n_max, int iters) {
+  if (batch < 1 || iters < 1) return 0;
+  return layout(nullptr, std::min(batch, SFM_MAX_BATCH), n_max, iters, nullptr);
+}
+
+int sfm_ransac5(const double* q, const double* qp, int64_t n, int num_test, int num_ransac_test, int iters,
+                double thr, uint64_t seed, int cheirality, void* workspace, size_t workspace_bytes,
+                double* E_out, double* P_out, int32_t* inliers_out, int32_t* winner_out, void* stream) {
+  SFM_REQUIRE(q && qp, "null point arrays");
+  SFM_REQUIRE(n >= 1, "need at least one correspondence");
+  SFM_REQUIRE(num_test >= 1 && num_ransac_test >= 1, "num_test_points and num_ransac_test_points must be >= 1");
+  const size_t need = layout(nullptr, 1, n, iters < 1 ? 1 : iters, nullptr);
+  if (!workspace || workspace_bytes < need) {
+    set_error("workspace too small: need " + std::to_string(need) + " bytes");
+    return SFM_ERR_WORKSPACE;
+  }
+  Workspace w;
+  layout((char*)workspace, 1, n, iters < 1 ? 1 : iters, &w);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, q, qp, n, w.pack);
+  SFM_LAUNCHED();
+  const int64_t nn[1] = {n};
+  return run_packed(w.pack, n, nn, 1, num_test, num_ransac_test, iters, thr, seed, cheirality, workspace,
+                    workspace_bytes, E_out, P_out, inliers_out, winner_out, nullptr, s);
+}
+
+int sfm_ransac5_packed(const double* pts, int64_t n_stride, const int64_t* n, int batch, int num_test,
+                       int num_ransac_test, int iters, double thr, uint64_t seed, int cheirality,
+                       void* workspace, size_t workspace_bytes, double* E_out, double* P_out,
+                       int32_t* inliers_out, int32_t* winner_out, int32_t* hyp_score_out, void* stream) {
+  return run_packed(pts, n_stride, n, batch, num_test, num_ransac_test, iters, thr, seed, cheirality, workspace,
+                    workspace_bytes, E_out, P_out, inliers_out, winner_out, hyp_score_out, (hipStream_t)stream);
+}
+
+int sfm_ransac5_inlier_mask(const double* pts, int64_t n_stride, const int64_t* n, int batch, const double* E,
+                            double thr, uint8_t* mask, void* stream) {
+  SFM_REQUIRE(pts && n && E && mask, "null pointer argument");
+  SFM_REQUIRE(batch >= 1, "batch must be >= 1");
+  hipStream_t s = (hipStream_t)stream;
+  for (int b0 = 0; b0 < batch; b0 += SFM_MAX_BATCH) {
+    const int nb = std::min(SFM_MAX_BATCH, batch - b0);
+    PairParams pp{};
+    for (int b = 0; b < nb; ++b) {
+      SFM_REQUIRE(n[b0 + b] >= 0 && n[b0 + b] <= n_stride, "n[b] must be in [0, n_stride]");
+      pp.n[b] = n[b0 + b];
+    }
+    hipLaunchKernelGGL(k_inlier_mask, dim3((unsigned)((n_stride + 255) / 256), nb), dim3(256), 0, s,
+                       pts + (size_t)b0 * n_stride * 4, n_stride, pp, E + (size_t)b0 * 9, thr,
+                       mask + (size_t)b0 * n_stride);
+    SFM_LAUNCHED();
+  }
+  return SFM_OK;
+}
+
+int sfm_ransac5_candidate_counts(const void* workspace, size_t workspace_bytes, int batch, int iters,
+                                 int32_t* counts_host) {
+  SFM_REQUIRE(workspace && counts_host && batch >= 1 && batch <= SFM_MAX_BATCH && iters >= 1, "invalid arguments");
+  const int bc = batch;
+  SFM_REQUIRE(workspace_bytes >= layout(nullptr, bc, 0, iters, nullptr), "workspace too small");
+  Workspace w;
+  layout((char*)workspace, bc, 0, iters, &w);
+  SFM_HIP(hipMemcpy(counts_host, w.cand_total, sizeof(int32_t) * batch, hipMemcpyDeviceToHost));
+  return SFM_OK;
+}
+
+int sfm_pack_points(const double* q, const double* qp, int64_t n, double* pts_out, void* stream) {
+  SFM_REQUIRE(q && qp && pts_out && n >= 0, "invalid arguments");
+  if (n == 0) return SFM_OK;
+  hipLaunchKernelGGL(k_pack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, q, qp, n,
+                     pts_out);
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+int sfm_flow_to_points(const float* flow, int batch, int H, int W, int h_side, int w_side, int margin,
+                       const float* Kinv, double* pts_out, void* stream) {
+  SFM_REQUIRE(flow && Kinv && pts_out, "null pointer argument");
+  SFM_REQUIRE(batch >= 1 && H >= 1 && W >= 1, "invalid flow shape");
+  SFM_REQUIRE(h_side >= 1 && h_side <= H && w_side >= 1 && w_side <= W, "h_side/w_side out of range");
+  SFM_REQUIRE(margin >= 0 && 2 * margin < h_side && 2 * margin < w_side, "margin leaves no pixels");
+  const int64_t N = (int64_t)(h_side - 2 * margin) * (w_side - 2 * margin);
+  hipStream_t s = (hipStream_t)stream;
+  for (int b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = std::min(65535, batch - b0);
+    ProfScope ps("flow_to_points", s);
+    hipLaunchKernelGGL(k_flow_points, dim3((unsigned)((N + 255) / 256), nb), dim3(256), 0, s,
+                       flow + (size_t)b0 * 2 * H * W, H, W, h_side, w_side, margin, Kinv + (size_t)b0 * 9,
+                       pts_out + (size_t)b0 * N * 4);
+  }
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+"""The measured hot path: dense flow -> RANSAC five-point pose -> plane sweep.
+
+``TwoViewHotPath`` runs, for a batch of image pairs already resident on the
+GPU, exactly the work SFMnet.forward does between the flow estimator and the
+3-D cost-regularisation CNN (models/SFMnet.py:103-166 with the dense-flow
+branch of pose_by_ransac 176-274, and PSNet.py:130-158):
+
+  1. correspondences from the flow (margin 10, K^-1)      sfm_flow_to_points
+  2. RANSAC five-point E / P per pair (H = 512 x iters)    sfm_ransac5_packed
+  3. P -> pose, optional RESCALE_DEPTH translation scaling
+  4. cost volume [B, 2C, L, h, w] at quarter resolution    sfm_plane_sweep
+
+All buffers (points, RANSAC workspace, cost volume) are allocated once and
+reused, so a step launches kernels only (hipGraph-capturable).
+"""
+import torch
+
+from . import ransac, sweep
+
+
+class TwoViewHotPath:
+    def __init__(self, batch, image_hw, feat_hw, channels=32, nlabel=128, iters=8, threshold=1e-4,
+                 min_depth=1.0, rescale_depth=False, norm_target=0.6, cost_dtype=torch.float32, margin=10,
+                 device="cuda", seed=ransac.DEFAULT_SEED):
+        self.batch = int(batch)
+        self.H, self.W = image_hw
+        self.h, self.w = feat_hw
+        self.C = int(channels)
+        self.L = int(nlabel)
+        self.iters = int(iters)
+        self.thr = float(threshold)
+        self.min_depth = float(min_depth)
+        self.rescale = float(norm_target) if rescale_depth else None
+        self.margin = int(margin)
+        self.seed = int(seed)
+        self.device = torch.device(device)
+        self.n = (self.H - 2 * margin) * (self.W - 2 * margin)
+        B = self.batch
+        self.pts = torch.empty(B, self.n, 4, dtype=torch.float64, device=self.device)
+        self.ws = ransac.workspace_for(B, self.iters, self.device)
+        self.cost = torch.empty(B, 2 * self.C, self.L, self.h, self.w, dtype=cost_dtype, device=self.device)
+        self.cost_dtype = cost_dtype
+
+    def pose(self, flow, K):
+        Kinv = torch.inverse(K.float())
+        ransac.flow_to_points(flow, Kinv, self.H, self.W, self.margin, out=self.pts)
+        E, P, inl, win = ransac.ransac5_batched(self.pts, None, None, None, self.iters, self.thr, self.seed,
+                                                True, workspace=self.ws)
+        return E, P, inl, win
+
+    def sweep(self, ref_fea, tgt_fea, P, K):
+        Kinv = torch.inverse(K.float())
+        K4, Ki4 = sweep.quarter_intrinsics(K.float(), Kinv)
+        pose = P.float()
+        if self.rescale is not None:
+            pose[:, :, -1:] = pose[:, :, -1:] * self.rescale
+        return sweep.plane_sweep_cost(ref_fea, tgt_fea, pose, K4, Ki4, self.L, self.min_depth, self.cost_dtype,
+                                      out=self.cost)
+
+    def step(self, flow, K, ref_fea, tgt_fea):
+        E, P, inl, win = self.pose(flow, K)
+        cost = self.sweep(ref_fea, tgt_fea, P, K)
+        return E, P, inl, cost

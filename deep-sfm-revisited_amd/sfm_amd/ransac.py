@@ -1,0 +1,152 @@
+"""Torch-facing RANSAC five-point entry points over the C ABI.
+
+Reference semantics: RANSAC_FiveP/essential_matrix/essential_matrix.cu:110-280
+(host drivers) and kernel_functions.cu:53-226 (kernels); see include/sfm_hip.h
+for the exact selection rules and the canonical handling of the reference's
+indeterminate cases.
+"""
+import torch
+
+from . import _lib
+
+CHAINS = 512          # reference: 8 blocks x 64 threads (essential_matrix.cu:201-203)
+DEFAULT_SEED = 1234   # essential_matrix.cu:15
+
+
+def _check_dev_f64(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+    if t.dtype != torch.float64:
+        raise RuntimeError(f"{name} must be a double tensor")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+
+
+def hypotheses(iters):
+    return CHAINS * int(iters)
+
+
+def _workspace(batch, n_max, iters, device):
+    nbytes = _lib.load().sfm_ransac5_workspace_bytes(int(batch), int(n_max), int(iters))
+    if nbytes == 0:
+        raise RuntimeError("invalid RANSAC workspace request")
+    return torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+
+
+def ransac5(q, qp, num_test_points, num_ransac_test_points, iters, threshold, seed=DEFAULT_SEED,
+            cheirality=True):
+    """One pair, reference layout: q, qp [N,2] float64 CUDA contiguous.
+    Returns (E [3,3] f64, P [3,4] f64 or None, inliers int32[1], winner int32[1])
+    — all on the device, nothing synchronises."""
+    _check_dev_f64(q, "input1")
+    _check_dev_f64(qp, "input2")
+    if q.dim() != 2 or q.shape[1] != 2 or qp.shape != q.shape:
+        raise RuntimeError("input1/input2 must both be [N, 2]")
+    n = q.shape[0]
+    dev = q.device
+    with torch.cuda.device(dev):
+        ws = _workspace(1, n, iters, dev)
+        E = torch.empty(3, 3, dtype=torch.float64, device=dev)
+        P = torch.empty(3, 4, dtype=torch.float64, device=dev) if cheirality else None
+        inl = torch.empty(1, dtype=torch.int32, device=dev)
+        win = torch.empty(1, dtype=torch.int32, device=dev)
+        rc = _lib.load().sfm_ransac5(_lib.ptr(q), _lib.ptr(qp), n, int(num_test_points),
+                                     int(num_ransac_test_points), int(iters), float(threshold), int(seed),
+                                     1 if cheirality else 0, _lib.ptr(ws), ws.numel(), _lib.ptr(E), _lib.ptr(P),
+                                     _lib.ptr(inl), _lib.ptr(win), _lib.stream_ptr(dev))
+        _lib.check(rc, "sfm_ransac5")
+    return E, P, inl, win
+
+
+def ransac5_batched(pts, n=None, num_test_points=None, num_ransac_test_points=None, iters=5, threshold=1e-4,
+                    seed=DEFAULT_SEED, cheirality=True, return_scores=False, workspace=None):
+    """Batched pairs on packed correspondences pts [B, Nstride, 4] float64
+    (x, y, x', y').  ``n``: points per pair (default: all Nstride).  Returns
+    (E [B,3,3], P [B,3,4] or None, inliers [B] int32, winner [B] int32[, scores [B,H]])."""
+    _check_dev_f64(pts, "pts")
+    if pts.dim() != 3 or pts.shape[2] != 4:
+        raise RuntimeError("pts must be [B, N, 4]")
+    B, ns, _ = pts.shape
+    n = [ns] * B if n is None else [int(v) for v in n]
+    if len(n) != B:
+        raise RuntimeError("len(n) must equal the batch size")
+    dev = pts.device
+    H = hypotheses(iters)
+    with torch.cuda.device(dev):
+        if workspace is None:
+            workspace = _workspace(B, 0, iters, dev)
+        E = torch.empty(B, 3, 3, dtype=torch.float64, device=dev)
+        P = torch.empty(B, 3, 4, dtype=torch.float64, device=dev) if cheirality else None
+        inl = torch.empty(B, dtype=torch.int32, device=dev)
+        win = torch.empty(B, dtype=torch.int32, device=dev)
+        scores = torch.empty(B, H, dtype=torch.int32, device=dev) if return_scores else None
+        rc = _lib.load().sfm_ransac5_packed(
+            _lib.ptr(pts), ns, _lib.i64_array(n), B, int(num_test_points or 0), int(num_ransac_test_points or 0),
+            int(iters), float(threshold), int(seed), 1 if cheirality else 0, _lib.ptr(workspace),
+            workspace.numel(), _lib.ptr(E), _lib.ptr(P), _lib.ptr(inl), _lib.ptr(win), _lib.ptr(scores),
+            _lib.stream_ptr(dev))
+        _lib.check(rc, "sfm_ransac5_packed")
+    out = (E, P, inl, win)
+    return out + (scores,) if return_scores else out
+
+
+def workspace_for(batch, iters, device):
+    """Pre-allocate a reusable workspace for ransac5_batched (graph capture)."""
+    return _workspace(batch, 0, iters, device)
+
+
+def pack_points(q, qp):
+    """q, qp [N,2] float64 CUDA -> pts [1, N, 4]."""
+    _check_dev_f64(q, "input1")
+    _check_dev_f64(qp, "input2")
+    n = q.shape[0]
+    out = torch.empty(1, n, 4, dtype=torch.float64, device=q.device)
+    with torch.cuda.device(q.device):
+        _lib.check(_lib.load().sfm_pack_points(_lib.ptr(q), _lib.ptr(qp), n, _lib.ptr(out),
+                                               _lib.stream_ptr(q.device)), "sfm_pack_points")
+    return out
+
+
+def inlier_mask(pts, E, threshold, n=None):
+    """Exact inlier mask [B, Nstride] (bool) of E [B,3,3] over packed points."""
+    _check_dev_f64(pts, "pts")
+    B, ns, _ = pts.shape
+    n = [ns] * B if n is None else [int(v) for v in n]
+    E = E.reshape(B, 9).contiguous().to(torch.float64)
+    mask = torch.empty(B, ns, dtype=torch.uint8, device=pts.device)
+    with torch.cuda.device(pts.device):
+        _lib.check(_lib.load().sfm_ransac5_inlier_mask(_lib.ptr(pts), ns, _lib.i64_array(n), B, _lib.ptr(E),
+                                                       float(threshold), _lib.ptr(mask),
+                                                       _lib.stream_ptr(pts.device)), "sfm_ransac5_inlier_mask")
+    return mask.bool()
+
+
+def flow_to_points(flow, intrinsic_inv, h_side=None, w_side=None, margin=10, out=None):
+    """Dense correspondences of SFMnet.pose_by_ransac (models/SFMnet.py:179-263):
+    flow [B,2,H,W] float32, intrinsic_inv [B,3,3] float32 (CUDA) -> pts [B,N,4]
+    float64 with N = (h_side-2m)(w_side-2m)."""
+    if not flow.is_cuda:
+        raise RuntimeError("flow must be a CUDA tensor")
+    flow = flow.contiguous().float()
+    Ki = intrinsic_inv.contiguous().float()
+    B, _, H, W = flow.shape
+    h = H if h_side is None else int(h_side)
+    w = W if w_side is None else int(w_side)
+    N = (h - 2 * margin) * (w - 2 * margin)
+    if out is None:
+        out = torch.empty(B, N, 4, dtype=torch.float64, device=flow.device)
+    with torch.cuda.device(flow.device):
+        _lib.check(_lib.load().sfm_flow_to_points(_lib.ptr(flow), B, H, W, h, w, int(margin), _lib.ptr(Ki),
+                                                  _lib.ptr(out), _lib.stream_ptr(flow.device)),
+                   "sfm_flow_to_points")
+    return out
+
+
+def candidate_counts(workspace, batch, iters):
+    """Per-pair number of candidate E's scored by the last ransac5_batched call
+    that used ``workspace`` (synchronises)."""
+    import ctypes
+    out = (ctypes.c_int32 * int(batch))()
+    _lib.check(_lib.load().sfm_ransac5_candidate_counts(_lib.ptr(workspace), workspace.numel(), int(batch),
+                                                        int(iters), out), "sfm_ransac5_candidate_counts")
+    return [int(v) for v in out]

@@ -1,0 +1,109 @@
+"""Plane-sweep stage over the C ABI.
+
+* ``plane_sweep_cost`` — replaces the per-plane loop of models/PSNet.py:144-157
+  (cost[:, :C, i] = ref, cost[:, C:, i] = inverse_warp(tgt, d_i)) with one
+  kernel launch.
+* ``inverse_warp``     — drop-in for models/inverse_warp.py:121-153.
+* ``PlaneSweep``       — the sweep section of PSNet.forward (PSNet.py:130-158):
+  K/4 rows 0-1, K^-1[:2,:2]*4, optional RESCALE_DEPTH translation scaling (in
+  place on the caller's pose tensor, as the reference does), one cost volume
+  per target view.
+"""
+import torch
+
+from . import _lib
+
+
+def _dev_f32(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+    return t.contiguous().float()
+
+
+def check_sizes(t, name, expected):
+    """models/inverse_warp.py:19-24"""
+    ok = t.dim() == len(expected) and all(
+        (not s.isdigit()) or t.size(i) == int(s) for i, s in enumerate(expected))
+    assert ok, "wrong size for {}, expected {}, got  {}".format(name, "x".join(expected), list(t.size()))
+
+
+def plane_sweep_cost(ref_fea, tgt_fea, pose, intrinsics4, intrinsics_inv4, nlabel, min_depth=1.0,
+                     dtype=torch.float32, out=None, warped_only=False):
+    """Cost volume [B, 2C, L, h, w] (or [B, C, L, h, w] with warped_only).
+    ``pose`` [B,3,4] (already translation-rescaled), intrinsics at feature
+    resolution.  ``dtype``: torch.float32 or torch.bfloat16."""
+    tgt = _dev_f32(tgt_fea, "tgt_fea")
+    B, C, h, w = tgt.shape
+    ref = None if warped_only else _dev_f32(ref_fea, "ref_fea")
+    pose = _dev_f32(pose.reshape(B, 3, 4), "pose")
+    K4 = _dev_f32(intrinsics4.reshape(B, 3, 3), "intrinsics")
+    Ki4 = _dev_f32(intrinsics_inv4.reshape(B, 3, 3), "intrinsics_inv")
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise RuntimeError("cost dtype must be float32 or bfloat16")
+    cout = C if warped_only else 2 * C
+    if out is None:
+        out = torch.empty(B, cout, int(nlabel), h, w, dtype=dtype, device=tgt.device)
+    code = 0 if dtype == torch.float32 else 1
+    L = _lib.load()
+    with torch.cuda.device(tgt.device):
+        s = _lib.stream_ptr(tgt.device)
+        if warped_only:
+            rc = L.sfm_plane_sweep_warped(_lib.ptr(tgt), B, C, h, w, _lib.ptr(pose), _lib.ptr(K4), _lib.ptr(Ki4),
+                                          int(nlabel), float(min_depth), code, _lib.ptr(out), s)
+        else:
+            rc = L.sfm_plane_sweep(_lib.ptr(ref), _lib.ptr(tgt), B, C, h, w, _lib.ptr(pose), _lib.ptr(K4),
+                                   _lib.ptr(Ki4), int(nlabel), float(min_depth), code, _lib.ptr(out), s)
+        _lib.check(rc, "sfm_plane_sweep")
+    return out
+
+
+def inverse_warp(feat, depth, pose, intrinsics, intrinsics_inv, padding_mode="zeros"):
+    """models/inverse_warp.py:121-153 (bilinear, zeros padding, align_corners=True)."""
+    check_sizes(depth, "depth", "BHW")
+    check_sizes(pose, "pose", "B34")
+    check_sizes(intrinsics, "intrinsics", "B33")
+    check_sizes(intrinsics_inv, "intrinsics", "B33")
+    assert intrinsics_inv.size() == intrinsics.size()
+    if padding_mode != "zeros":
+        raise NotImplementedError("only padding_mode='zeros' is on the plane-sweep path")
+    f = _dev_f32(feat, "feat")
+    B, C, h, w = f.shape
+    d = _dev_f32(depth, "depth")
+    out = torch.empty_like(f)
+    with torch.cuda.device(f.device):
+        rc = _lib.load().sfm_inverse_warp(_lib.ptr(f), B, C, h, w, _lib.ptr(d), _lib.ptr(_dev_f32(pose, "pose")),
+                                          _lib.ptr(_dev_f32(intrinsics, "intrinsics")),
+                                          _lib.ptr(_dev_f32(intrinsics_inv, "intrinsics_inv")), _lib.ptr(out),
+                                          _lib.stream_ptr(f.device))
+        _lib.check(rc, "sfm_inverse_warp")
+    return out
+
+
+def quarter_intrinsics(intrinsics, intrinsics_inv):
+    """PSNet.py:130-133: K/4 on rows 0-1; K^-1 with [:2,:2]*4."""
+    K4 = intrinsics.clone()
+    Ki4 = intrinsics_inv.clone()
+    K4[:, :2, :] = K4[:, :2, :] / 4
+    Ki4[:, :2, :2] = Ki4[:, :2, :2] * 4
+    return K4, Ki4
+
+
+class PlaneSweep(torch.nn.Module):
+    """Sweep section of PSNet.forward (models/PSNet.py:128-158) on given features."""
+
+    def __init__(self, nlabel, mindepth=1.0, rescale_depth=False, norm_target=0.8, dtype=torch.float32):
+        super().__init__()
+        self.nlabel = int(nlabel)
+        self.mindepth = float(mindepth)
+        self.rescale_depth = rescale_depth
+        self.norm_target = norm_target
+        self.dtype = dtype
+
+    def forward(self, ref_fea, tgt_feas, pose, intrinsics, intrinsics_inv):
+        """ref_fea [B,C,h,w]; tgt_feas list of [B,C,h,w]; pose [B,T,3,4];
+        returns a list of cost volumes [B,2C,L,h,w]."""
+        K4, Ki4 = quarter_intrinsics(intrinsics, intrinsics_inv)
+        if self.rescale_depth:
+            pose[:, 0, :, -1:] = pose[:, 0, :, -1:] * self.norm_target
+        return [plane_sweep_cost(ref_fea, t, pose[:, j], K4, Ki4, self.nlabel, self.mindepth, self.dtype)
+                for j, t in enumerate(tgt_feas)]

@@ -1,0 +1,182 @@
+/*
+ * sfm_hip.h — C ABI of the MI355X-native two-view SfM hot path
+ * (libsfm_hip.so, built from deep-sfm-revisited_amd/csrc for gfx950).
+ *
+ * Drop-in boundary for jytime/Deep-SfM-Revisited:
+ *   - the `essential_matrix` PyTorch extension (RANSAC_FiveP/essential_matrix/
+ *     essential_matrix_wrapper.cpp:102-108) — initialise / computeP / optimise /
+ *     decompose / decomposeUV;
+ *   - the plane-sweep cost volume of models/PSNet.py:144-158 and the per-plane
+ *     warp models/inverse_warp.py:121-153;
+ *   - the dense correspondence build of models/SFMnet.py:176-263 (flow2coord
+ *     298-318) feeding the RANSAC.
+ *
+ * Conventions
+ *   - Every pointer marked [dev] is device memory on the current HIP device;
+ *     [host] is host memory.  No torch types cross this boundary.
+ *   - Device work is stream-ordered on `stream` (a hipStream_t, NULL = default
+ *     stream).  Functions return before the work completes unless stated.
+ *   - Return value: SFM_OK (0) or an SFM_ERR_* code; sfm_last_error() gives a
+ *     message (thread-local).  Nothing calls exit() (the reference's
+ *     CudaErrorCheck exit()s the process: essential_matrix.cu:17-24).
+ *   - Scratch memory is caller-provided (`workspace`), sized by the matching
+ *     *_workspace_bytes() query; no call allocates device memory, so every
+ *     device entry point is hipGraph-capturable.
+ */
+#ifndef SFM_HIP_H
+#define SFM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  SFM_OK = 0,
+  SFM_ERR_ARG = 1,        /* invalid argument (shape, size, range)          */
+  SFM_ERR_HIP = 2,        /* HIP runtime / launch error                     */
+  SFM_ERR_WORKSPACE = 3   /* workspace missing or too small                 */
+};
+
+#define SFM_ABI_VERSION 1
+#define SFM_RANSAC_CHAINS 512   /* reference: 8 blocks x 64 threads (essential_matrix.cu:201-203) */
+#define SFM_MAX_BATCH 64        /* pairs per device launch (larger batches are chunked) */
+
+int sfm_abi_version(void);
+const char* sfm_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * RANSAC five-point essential matrix
+ * ------------------------------------------------------------------------
+ * Hypotheses: H = SFM_RANSAC_CHAINS * iters; hypothesis h = t*iters + i is
+ * iteration i of chain t (reference thread t).  Sampling: Philox4x32-10 keyed
+ * by `seed`, counter {h, draw/4, 0, 0}, curand_uniform-style (0,1] floats
+ * turned into indices by the reference's RandomInt arithmetic, clamped to n-1.
+ * Selection: per hypothesis the best candidate on the first num_test points
+ * (first strict max, default candidate 0), rescored on the first
+ * num_ransac_test points; the winner is the first hypothesis (in h order)
+ * with the maximal rescored count — exactly the reference's per-thread
+ * strict-> update followed by the host max_element (kernel_functions.cu:
+ * 141-226, essential_matrix.cu:248-265).  If no hypothesis has an inlier,
+ * E = P = 0, inliers = 0, winner = -1 (the reference returns uninitialised
+ * memory there).
+ */
+
+/* Workspace for up to `batch` pairs of at most n_max points and `iters`
+ * RANSAC iterations per chain. */
+size_t sfm_ransac5_workspace_bytes(int batch, int64_t n_max, int iters);
+
+/* Single pair, reference layout.  Replaces ProjectionMatrixRansac
+ * (essential_matrix.cu:190-280, cheirality=1) and EssentialMatrixInitialise
+ * (essential_matrix.cu:110-184, cheirality=0).
+ *   q, qp          [dev] n x 2 float64, row-major (x, y) — input1 / input2
+ *   E_out          [dev] 3x3 float64; P_out [dev] 3x4 float64 (may be NULL
+ *                  when cheirality == 0); inliers_out [dev] int32[1];
+ *   winner_out     [dev] int32[1] or NULL.
+ * Requires 1 <= num_test, num_ransac_test <= n (the reference reads out of
+ * bounds otherwise), iters >= 1, thr > 0. */
+int sfm_ransac5(const double* q, const double* qp, int64_t n,
+                int num_test, int num_ransac_test, int iters, double thr,
+                uint64_t seed, int cheirality,
+                void* workspace, size_t workspace_bytes,
+                double* E_out, double* P_out, int32_t* inliers_out, int32_t* winner_out,
+                void* stream);
+
+/* Batched pairs on packed correspondences.
+ *   pts            [dev] batch x n_stride x 4 float64: (x, y, x', y') per point
+ *   n              [host] batch int64: points of each pair (<= n_stride)
+ *   num_test, num_ransac_test: per-call; values <= 0 mean "all n[b] points"
+ *   E_out [dev] batch x 9, P_out [dev] batch x 12 (or NULL), inliers_out
+ *   [dev] batch int32, winner_out [dev] batch int32 or NULL,
+ *   hyp_score_out  [dev] batch x H int32 rescored count per hypothesis, or NULL.
+ */
+int sfm_ransac5_packed(const double* pts, int64_t n_stride, const int64_t* n, int batch,
+                       int num_test, int num_ransac_test, int iters, double thr,
+                       uint64_t seed, int cheirality,
+                       void* workspace, size_t workspace_bytes,
+                       double* E_out, double* P_out, int32_t* inliers_out, int32_t* winner_out,
+                       int32_t* hyp_score_out, void* stream);
+
+/* Exact inlier mask of E (reference ComputeError + `<= thr`) for each point.
+ *   pts [dev] batch x n_stride x 4; n [host] batch; E [dev] batch x 9;
+ *   mask [dev] batch x n_stride uint8 (entries >= n[b] are written 0). */
+int sfm_ransac5_inlier_mask(const double* pts, int64_t n_stride, const int64_t* n, int batch,
+                            const double* E, double thr, uint8_t* mask, void* stream);
+
+/* Dense flow -> packed normalised correspondences (models/SFMnet.py:179-263,
+ * flow2coord 298-318): crop flow to h_side x w_side, drop a `margin` border,
+ * q = (K^-1 (u, v, 1))[:2], qp = (K^-1 (u+fu, v+fv, 1))[:2] in float32 rows
+ * (k0*x + k1*y) + k2, widened to float64.  Point k = (v-m)*(w_side-2m)+(u-m).
+ *   flow [dev] batch x 2 x H x W float32; Kinv [dev] batch x 3 x 3 float32;
+ *   pts_out [dev] batch x N x 4 float64, N = (h_side-2m)(w_side-2m). */
+int sfm_flow_to_points(const float* flow, int batch, int H, int W, int h_side, int w_side,
+                       int margin, const float* Kinv, double* pts_out, void* stream);
+
+/* Scored candidate E's per pair of the last sfm_ransac5_packed call made with
+ * this workspace (the last <= SFM_MAX_BATCH chunk), copied to the host
+ * (synchronous).  Work accounting: the score kernel evaluates
+ * counts[b] x max(num_test, num_ransac_test) correspondences for pair b. */
+int sfm_ransac5_candidate_counts(const void* workspace, size_t workspace_bytes, int batch, int iters,
+                                 int32_t* counts_host);
+
+/* Pack reference-layout q, qp (n x 2 each) into pts (n x 4). */
+int sfm_pack_points(const double* q, const double* qp, int64_t n, double* pts_out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Host-side E utilities (the reference runs these on CPU tensors too)
+ * ------------------------------------------------------------------------ */
+/* EssentialMatrixOptimise -> polish_E_robust_parametric (essential_matrix.cu:
+ * 76-105, polish_E.cu:1470-1577).  All pointers [host]; q, qp n x 2. */
+int sfm_essential_optimise(const double* q, const double* qp, int64_t n, const double* E_init,
+                           double delta, double alpha, int max_reps, double* E_out);
+/* EssentialMatrixDecompose -> Edecomp(E, params) (essential_matrix.cu:29-43). */
+int sfm_essential_decompose(const double* E, double* params5);
+/* EssentialMatrixDecomposeUV -> Edecomp(E, U, V) (essential_matrix.cu:48-70). */
+int sfm_essential_decompose_uv(const double* E, double* U, double* V);
+
+/* ------------------------------------------------------------------------
+ * Plane sweep
+ * ------------------------------------------------------------------------ */
+/* Cost volume of models/PSNet.py:144-157 for one target view:
+ *   cost[b, c,   i] = ref[b, c]                     (c < C)
+ *   cost[b, C+c, i] = inverse_warp(tgt, d_i)[b, c]
+ * with d_i = (min_depth * nlabel) / (i + 1) in float32.
+ *   ref, tgt [dev] batch x C x h x w float32
+ *   pose     [dev] batch x 3 x 4 float32 (already RESCALE_DEPTH-scaled)
+ *   K4, K4inv [dev] batch x 3 x 3 float32 (feature-resolution intrinsics)
+ *   out_dtype 0: float32, 1: bfloat16 (round-to-nearest-even)
+ *   cost     [dev] batch x 2C x nlabel x h x w */
+int sfm_plane_sweep(const float* ref, const float* tgt, int batch, int channels, int h, int w,
+                    const float* pose, const float* K4, const float* K4inv,
+                    int nlabel, float min_depth, int out_dtype, void* cost, void* stream);
+
+/* Warped half only (cost[b, c, i] = inverse_warp(tgt, d_i)), batch x C x nlabel x h x w. */
+int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w,
+                           const float* pose, const float* K4, const float* K4inv,
+                           int nlabel, float min_depth, int out_dtype, void* out, void* stream);
+
+/* models/inverse_warp.py:121-153 for an arbitrary depth map:
+ *   feat [dev] B x C x h x w; depth [dev] B x h x w; pose [dev] B x 3 x 4;
+ *   K, Kinv [dev] B x 3 x 3; out [dev] B x C x h x w (float32). */
+int sfm_inverse_warp(const float* feat, int batch, int channels, int h, int w,
+                     const float* depth, const float* pose, const float* K, const float* Kinv,
+                     float* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Per-kernel timing (HIP events recorded around every launch on the
+ * launching stream while enabled).
+ * ------------------------------------------------------------------------ */
+int sfm_profile_enable(int on);
+int sfm_profile_reset(void);
+/* Synchronises the recorded events; total milliseconds and launch count of
+ * kernel `name` ("ransac_solve", "ransac_chain", "ransac_score",
+ * "ransac_select", "flow_to_points", "plane_sweep", ...). */
+int sfm_profile_read(const char* name, double* total_ms, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SFM_HIP_H */

@@ -1,0 +1,244 @@
+"""Generate tests/golden/*.npz from the REFERENCE's own code (test infrastructure).
+
+Run in the survey container, where /root/reference exists:
+    make -C oracle all ref && python -m oracle.gen_golden
+
+* RANSAC fixtures come from oracle/_ref/libref_ransac.so: the reference's
+  essential_matrix_5pt.cu / sturm.cu / cheirality.cu / polish_E.cu compiled
+  in place with g++ (oracle/Makefile), with the CUDA kernel loop restated
+  around them (oracle/ref_harness.cpp) and the build's specified sampler.
+* Warp / cost-volume / Flow2Depth fixtures come from importing
+  /root/reference/models/inverse_warp.py and models/flow2depth.py on the CPU
+  (their `.cuda()` calls are made no-ops for the duration of the call).
+  The PSNet loop around inverse_warp (PSNet.py:144-157) is restated here.
+
+Only inputs and outputs are written (no reference source).
+"""
+import importlib.util
+import os
+
+import numpy as np
+import torch
+
+from . import ransac5 as R
+
+REF = "/root/reference"
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
+
+
+def _load_ref_module(rel, name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, rel))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+class _NoCuda:
+    def __enter__(self):
+        self.orig = torch.Tensor.cuda
+        torch.Tensor.cuda = lambda t, *a, **k: t
+        return self
+
+    def __exit__(self, *a):
+        torch.Tensor.cuda = self.orig
+
+
+def geometric_scene(rng, n, out_frac=0.15, noise=0.002, depth=(2.0, 40.0)):
+    """Normalised-coordinate correspondences of a random rigid scene (numpy)."""
+    w = rng.normal(0, 0.03, 3)
+    th = np.linalg.norm(w)
+    k = w / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    Rm = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+    t = rng.normal(0, 0.3, 3)
+    t[2] = -abs(t[2]) - 0.8
+    X = np.stack([rng.uniform(-0.8, 0.8, n), rng.uniform(-0.3, 0.3, n), np.ones(n)], 1)
+    X = X * rng.uniform(depth[0], depth[1], (n, 1))
+    X2 = X @ Rm.T + t
+    q = X[:, :2] / X[:, 2:]
+    qp = X2[:, :2] / X2[:, 2:] + rng.normal(0, noise, (n, 2))
+    m = int(n * out_frac)
+    idx = rng.choice(n, m, replace=False)
+    qp[idx] = rng.uniform(-0.8, 0.8, (m, 2))
+    return q, qp
+
+
+def gen_solve5(rng):
+    qs, qps = [], []
+    for _ in range(600):
+        qs.append(rng.uniform(-1, 1, (5, 2)))
+        qps.append(rng.uniform(-1, 1, (5, 2)))
+    for _ in range(200):
+        q, qp = geometric_scene(rng, 5, out_frac=0.0, noise=0.0)
+        qs.append(q); qps.append(qp)
+    # degenerate tuples: repeated points, all-equal, collinear, pure rotation-ish
+    for _ in range(20):
+        q = rng.uniform(-1, 1, (5, 2)); qp = rng.uniform(-1, 1, (5, 2))
+        q[1] = q[0]; qp[1] = qp[0]
+        qs.append(q); qps.append(qp)
+    for _ in range(5):
+        a = rng.uniform(-1, 1, 2)
+        qs.append(np.tile(a, (5, 1))); qps.append(np.tile(rng.uniform(-1, 1, 2), (5, 1)))
+    for _ in range(10):
+        tt = rng.uniform(-1, 1, 5)
+        qs.append(np.stack([tt, 0.5 * tt + 0.1], 1)); qps.append(np.stack([tt + 0.01, 0.5 * tt + 0.12], 1))
+    for _ in range(10):
+        q = rng.uniform(-1, 1, (5, 2))
+        qs.append(q); qps.append(q + 1e-9 * rng.normal(size=(5, 2)))
+    q5 = np.stack(qs); qp5 = np.stack(qps)
+    M = len(q5)
+    out = dict(q5=q5, qp5=qp5, nroots=np.zeros(M, np.int32), nP=np.zeros(M, np.int32),
+               E_roots=np.zeros((M, 10, 9)), E=np.zeros((M, 10, 9)), P=np.zeros((M, 10, 12)),
+               nroots_nc=np.zeros(M, np.int32), E_nc=np.zeros((M, 10, 9)))
+    for i in range(M):
+        r = R.ref_solve5(q5[i], qp5[i], cheir=True)
+        out["nroots"][i] = r["nroots"]; out["nP"][i] = r["nP"]
+        out["E_roots"][i] = r["E_roots"]; out["E"][i] = r["E"]; out["P"][i] = r["P"]
+        r2 = R.ref_solve5(q5[i], qp5[i], cheir=False)
+        out["nroots_nc"][i] = r2["nroots"]; out["E_nc"][i] = r2["E"]
+    return out
+
+
+RANSAC_CASES = [
+    # name, n, num_test, num_ransac_test, iters, thr, cheir, out_frac, noise
+    ("dense_tr_equal", 2000, 2000, 2000, 2, 1e-3, True, 0.15, 0.002),
+    ("harness_style", 3000, 10, 1000, 1, 5e-2, True, 0.10, 0.01),
+    ("no_cheirality", 1500, 1500, 1500, 3, 1e-3, False, 0.20, 0.002),
+    ("tight_threshold", 1200, 1200, 1200, 4, 1e-4, True, 0.15, 0.001),
+    ("test_gt_ransac", 2500, 1800, 900, 2, 2e-3, True, 0.30, 0.003),
+    ("tiny_n", 7, 7, 7, 2, 1e-2, True, 0.0, 0.0),
+]
+
+
+def gen_ransac(rng):
+    out = {}
+    for (name, n, nt, nr, it, thr, cheir, of, noise) in RANSAC_CASES:
+        q, qp = geometric_scene(rng, n, out_frac=of, noise=noise)
+        r = R.ransac5(q, qp, nt, nr, it, thr, seed=1234, cheir=cheir, use_ref=True)
+        mask = R.inlier_mask(r["E"], q, qp, thr)
+        out[name] = dict(q=q, qp=qp, params=np.array([n, nt, nr, it, thr, int(cheir), 1234], dtype=np.float64),
+                         E=r["E"], P=r["P"], inliers=np.int32(r["inliers"]), winner=np.int32(r["winner"]),
+                         hyp_score=r["hyp_score"], hyp_ncand=r["hyp_ncand"], mask=mask)
+    return out
+
+
+def gen_irls(rng):
+    out = {}
+    for k in range(4):
+        q, qp = geometric_scene(rng, 800, out_frac=0.2, noise=0.002)
+        r = R.ransac5(q, qp, 800, 800, 2, 1e-3, seed=1234, cheir=True, use_ref=True)
+        E = r["E"]
+        out[f"case{k}"] = dict(q=q, qp=qp, E_init=E,
+                               E_opt=R.optimise(q, qp, E, 0.001, 0.0, 200, use_ref=True),
+                               E_opt_huber=R.optimise(q, qp, E, 0.002, 1.0, 20, use_ref=True),
+                               params=R.decompose(E, use_ref=True),
+                               U=R.decompose_uv(E, use_ref=True)[0], V=R.decompose_uv(E, use_ref=True)[1])
+    return out
+
+
+def gen_sampler():
+    seeds = [1234, 0, 2**40 + 7]
+    hs = np.arange(0, 4096, 37, dtype=np.uint32)
+    u32 = np.zeros((len(seeds), len(hs), 5), np.uint32)
+    idx = np.zeros((len(seeds), len(hs), 5, 3), np.int64)
+    ns = [7, 2000, 435032]
+    for a, s in enumerate(seeds):
+        for b, h in enumerate(hs):
+            for d in range(5):
+                u32[a, b, d] = R.philox_u32(s, int(h), d)
+                for c, n in enumerate(ns):
+                    idx[a, b, d, c] = R.sample_index(s, int(h), d, n)
+    return dict(seeds=np.array(seeds, np.uint64), hs=hs, ns=np.array(ns, np.int64), u32=u32, idx=idx)
+
+
+def gen_warp(rng):
+    iw = _load_ref_module("models/inverse_warp.py", "ref_inverse_warp")
+    f2d = _load_ref_module("models/flow2depth.py", "ref_flow2depth")
+    g = torch.Generator().manual_seed(3)
+    out = {}
+    B, C, h, w = 2, 4, 12, 20
+    K = torch.tensor([[[10.0, 0, 9.5], [0, 10.0, 5.5], [0, 0, 1]], [[12.0, 0, 10.0], [0, 11.0, 6.0], [0, 0, 1]]])
+    Ki = torch.inverse(K)
+    feat = torch.randn(B, C, h, w, generator=g)
+    cases = []
+    for k in range(6):
+        depth = 0.5 + 20 * torch.rand(B, h, w, generator=g)
+        ang = 0.3 * (torch.rand(B, 3, generator=g) - 0.5)
+        pose = torch.zeros(B, 3, 4)
+        for b in range(B):
+            a = ang[b]
+            Kx = torch.tensor([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+            pose[b, :, :3] = torch.matrix_exp(Kx)
+        pose[:, :, 3] = (torch.rand(B, 3, generator=g) - 0.5) * [0.5, 1.0, 2.0, 4.0, 8.0, 30.0][k]
+        cases.append((depth, pose))
+    with _NoCuda():
+        outs = [iw.inverse_warp(feat, d, p, K, Ki) for d, p in cases]
+    out["warp"] = dict(feat=feat.numpy(), K=K.numpy(), Kinv=Ki.numpy(),
+                       depth=torch.stack([d for d, _ in cases]).numpy(),
+                       pose=torch.stack([p for _, p in cases]).numpy(),
+                       out=torch.stack(outs).numpy())
+    # cost volume: PSNet.py:130-157 restated around the reference inverse_warp
+    Bc, Cc, hc, wc, L = 2, 8, 24, 40, 16
+    ref = torch.randn(Bc, Cc, hc, wc, generator=g)
+    tgt = torch.randn(Bc, Cc, hc, wc, generator=g)
+    Kf = torch.tensor([[[4 * 18.0, 0, 4 * 19.5], [0, 4 * 18.0, 4 * 11.5], [0, 0, 1]]]).repeat(Bc, 1, 1)
+    Kf[1, 0, 0] = 4 * 21.0
+    Kfi = torch.inverse(Kf)
+    K4 = Kf.clone(); Ki4 = Kfi.clone()
+    K4[:, :2, :] = K4[:, :2, :] / 4
+    Ki4[:, :2, :2] = Ki4[:, :2, :2] * 4
+    pose = torch.zeros(Bc, 3, 4)
+    pose[:, :, :3] = torch.eye(3)
+    pose[0, :, 3] = torch.tensor([0.1, -0.05, -1.0])
+    pose[1, :, :3] = torch.matrix_exp(torch.tensor([[0, -0.02, 0.01], [0.02, 0, -0.015], [-0.01, 0.015, 0.0]]))
+    pose[1, :, 3] = torch.tensor([-0.3, 0.02, -0.8])
+    pose_scaled = pose.clone()
+    pose_scaled[:, :, -1:] = pose_scaled[:, :, -1:] * 0.6      # RESCALE_DEPTH, NORM_TARGET 0.6
+    mindepth = 1.0
+    ones = torch.ones(Bc, hc, wc)
+    disp2depth = ones * mindepth * L
+    cost = torch.zeros(Bc, 2 * Cc, L, hc, wc)
+    with _NoCuda():
+        for i in range(L):
+            depth = torch.div(disp2depth, i + 1 + 1e-16)
+            cost[:, :Cc, i] = ref
+            cost[:, Cc:, i] = iw.inverse_warp(tgt, depth, pose_scaled, K4, Ki4)
+    out["cost"] = dict(ref=ref.numpy(), tgt=tgt.numpy(), K=Kf.numpy(), Kinv=Kfi.numpy(), pose=pose.numpy(),
+                       norm_target=np.float32(0.6), nlabel=np.int32(L), min_depth=np.float32(mindepth),
+                       cost=cost.numpy())
+    # Flow2Depth (dead code in the reference, restated for API completeness)
+    Rm = torch.matrix_exp(torch.tensor([[0, -0.05, 0.02], [0.05, 0, -0.01], [-0.02, 0.01, 0.0]])).unsqueeze(0)
+    T = torch.tensor([[0.1, -0.2, 0.9]])
+    Kd = torch.tensor([[[30.0, 0, 15.5], [0, 28.0, 9.5], [0, 0, 1]]])
+    flow = torch.zeros(1, 2, 9, 13)
+    with _NoCuda():
+        fd = f2d.Flow2Depth(Rm, T, flow, Kd)
+    out["flow2depth"] = dict(R=Rm.numpy(), T=T.numpy(), K=Kd.numpy(), shape=np.array([1, 2, 9, 13]), out=fd.numpy())
+    return out
+
+
+def _save(name, d):
+    flat = {}
+    for k, v in d.items():
+        if isinstance(v, dict):
+            for k2, v2 in v.items():
+                flat[f"{k}/{k2}"] = np.asarray(v2)
+        else:
+            flat[k] = np.asarray(v)
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **flat)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    rng = np.random.default_rng(20241015)
+    _save("solve5.npz", gen_solve5(rng))
+    _save("ransac.npz", gen_ransac(rng))
+    _save("irls.npz", gen_irls(rng))
+    _save("sampler.npz", gen_sampler())
+    _save("warp.npz", gen_warp(rng))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,136 @@
+"""HIP RANSAC five-point path vs the oracle / golden vectors (through the C ABI).
+
+Parity bar: bit-exact winning hypothesis, inlier count, per-hypothesis scores
+and inlier index set; E and P bit-exact as well (identical fp64 operation
+order; the root-scaling pow is correctly rounded on the device and glibc's on
+the host — a last-bit difference there would show as a failure here)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ransac5 as R
+from oracle import flow as OF
+
+pytestmark = pytest.mark.gpu
+
+
+def _ransac_gpu(q, qp, nt, nr, it, thr, cheir, dev, seed=1234):
+    from sfm_amd import ransac
+    qd = torch.from_numpy(np.ascontiguousarray(q)).to(dev)
+    qpd = torch.from_numpy(np.ascontiguousarray(qp)).to(dev)
+    pts = ransac.pack_points(qd, qpd)
+    E, P, inl, win, scores = ransac.ransac5_batched(pts, None, nt, nr, it, thr, seed, cheir, return_scores=True)
+    torch.cuda.synchronize()
+    mask = ransac.inlier_mask(pts, E, thr)[0].cpu().numpy()
+    return dict(E=E[0].cpu().numpy(), P=None if P is None else P[0].cpu().numpy(), inliers=int(inl[0]),
+                winner=int(win[0]), scores=scores[0].cpu().numpy(), mask=mask)
+
+
+@pytest.mark.parametrize("case", ["dense_tr_equal", "harness_style", "no_cheirality", "tight_threshold",
+                                  "test_gt_ransac", "tiny_n"])
+def test_ransac_golden(golden, cuda, case):
+    g = golden("ransac.npz")[case]
+    n, nt, nr, it, thr, cheir, seed = g["params"]
+    r = _ransac_gpu(g["q"], g["qp"], int(nt), int(nr), int(it), float(thr), bool(cheir), cuda, int(seed))
+    assert r["winner"] == int(g["winner"])
+    assert r["inliers"] == int(g["inliers"])
+    assert np.array_equal(r["scores"], g["hyp_score"])
+    assert np.array_equal(r["mask"], g["mask"])
+    assert np.array_equal(r["E"], g["E"])
+    if cheir:
+        assert np.array_equal(r["P"], g["P"])
+
+
+def test_essential_matrix_api(golden, cuda):
+    import essential_matrix
+    g = golden("ransac.npz")["dense_tr_equal"]
+    n, nt, nr, it, thr, cheir, seed = g["params"]
+    q = torch.from_numpy(g["q"]).to(cuda)
+    qp = torch.from_numpy(g["qp"]).to(cuda)
+    E, P, inl = essential_matrix.computeP(q, qp, int(nt), int(nr), int(it), float(thr))
+    assert E.shape == (3, 3) and P.shape == (3, 4) and E.dtype == torch.float64 and E.is_cuda
+    assert isinstance(inl, int) and inl == int(g["inliers"])
+    assert np.array_equal(E.cpu().numpy(), g["E"]) and np.array_equal(P.cpu().numpy(), g["P"])
+    E0 = essential_matrix.initialise(q, qp, int(nt), int(nr), int(it), float(thr))
+    ref = R.ransac5(g["q"], g["qp"], int(nt), int(nr), int(it), float(thr), cheir=False)
+    assert np.array_equal(E0.cpu().numpy(), ref["E"])
+    with pytest.raises(RuntimeError, match="CUDA"):
+        essential_matrix.computeP(q.cpu(), qp.cpu(), 10, 10, 1, 1e-3)
+    with pytest.raises(RuntimeError, match="double"):
+        essential_matrix.computeP(q.float(), qp.float(), 10, 10, 1, 1e-3)
+    with pytest.raises(RuntimeError, match="contiguous"):
+        essential_matrix.computeP(q.t().contiguous().t(), qp, 10, 10, 1, 1e-3)
+
+
+def _geom(rng, n, of=0.15, noise=0.002):
+    from oracle.gen_golden import geometric_scene
+    return geometric_scene(rng, n, out_frac=of, noise=noise)
+
+
+def test_batched_equals_single_calls(cuda):
+    from sfm_amd import ransac
+    rng = np.random.default_rng(5)
+    scenes = [_geom(rng, n) for n in (900, 1400, 700)]
+    ns = max(len(s[0]) for s in scenes)
+    pts = torch.zeros(3, ns, 4, dtype=torch.float64)
+    for b, (q, qp) in enumerate(scenes):
+        pts[b, : len(q)] = torch.from_numpy(np.c_[q, qp])
+    pts = pts.to(cuda)
+    E, P, inl, win = ransac.ransac5_batched(pts, [len(s[0]) for s in scenes], None, None, 3, 1e-3)
+    for b, (q, qp) in enumerate(scenes):
+        ref = R.ransac5(q, qp, len(q), len(q), 3, 1e-3)
+        assert int(win[b]) == ref["winner"] and int(inl[b]) == ref["inliers"]
+        assert np.array_equal(E[b].cpu().numpy(), ref["E"])
+        assert np.array_equal(P[b].cpu().numpy(), ref["P"])
+
+
+@pytest.mark.parametrize("thr", [5e-4, 3e-3, 2.0])   # 2.0 exercises the exact-only scoring kernel
+def test_threshold_paths(cuda, thr):
+    rng = np.random.default_rng(11)
+    q, qp = _geom(rng, 1500, of=0.3, noise=0.004)
+    r = _ransac_gpu(q, qp, 1500, 1500, 2, thr, True, cuda)
+    ref = R.ransac5(q, qp, 1500, 1500, 2, thr)
+    assert r["winner"] == ref["winner"] and r["inliers"] == ref["inliers"]
+    assert np.array_equal(r["scores"], ref["hyp_score"])
+
+
+def test_degenerate_inputs(cuda):
+    """Duplicate / constant correspondences: NaN solves, no inliers anywhere."""
+    q = np.tile(np.array([[0.1, -0.2]]), (40, 1))
+    qp = np.tile(np.array([[0.15, -0.1]]), (40, 1))
+    r = _ransac_gpu(q, qp, 40, 40, 1, 1e-3, True, cuda)
+    ref = R.ransac5(q, qp, 40, 40, 1, 1e-3)
+    assert r["winner"] == ref["winner"] and r["inliers"] == ref["inliers"]
+    assert np.array_equal(r["scores"], ref["hyp_score"])
+    if ref["winner"] < 0:
+        assert np.all(r["E"] == 0) and np.all(r["P"] == 0)
+
+
+def test_flow_to_points_matches_oracle(cuda):
+    from sfm_amd import ransac, synth
+    flow, K, pose, depth = synth.kitti_pair_batch(2, seed=3, hw=(60, 90))
+    Kinv = torch.inverse(K)
+    q, qp = OF.dense_correspondences(flow.numpy(), Kinv.numpy(), 56, 85, 10)
+    pts = ransac.flow_to_points(flow.to(cuda), Kinv.to(cuda), 56, 85, 10).cpu().numpy()
+    assert pts.shape == (2, (56 - 20) * (85 - 20), 4)
+    assert np.array_equal(pts[..., :2], q) and np.array_equal(pts[..., 2:], qp)
+
+
+def test_full_size_dense_pair(cuda):
+    """KITTI 376x1242 dense flow (N = 435,032): GPU vs oracle at H = 512."""
+    from sfm_amd import ransac, synth
+    flow, K, pose, depth = synth.kitti_pair_batch(1, seed=1)
+    Kinv = torch.inverse(K)
+    pts = ransac.flow_to_points(flow.to(cuda), Kinv.to(cuda))
+    assert pts.shape[1] == 435032
+    E, P, inl, win, scores = ransac.ransac5_batched(pts, None, None, None, 1, 1e-4, return_scores=True)
+    p = pts[0].cpu().numpy()
+    ref = R.ransac5(p[:, :2], p[:, 2:], 435032, 435032, 1, 1e-4, nthreads=16)
+    assert int(win[0]) == ref["winner"] and int(inl[0]) == ref["inliers"]
+    assert np.array_equal(scores[0].cpu().numpy(), ref["hyp_score"])
+    assert np.array_equal(E[0].cpu().numpy(), ref["E"])
+    m = ransac.inlier_mask(pts, E, 1e-4)[0].cpu().numpy()
+    assert np.array_equal(m, R.inlier_mask(ref["E"], p[:, :2], p[:, 2:], 1e-4))
+    # the recovered pose is the true one up to the translation scale
+    t = P[0, :, 3].cpu().numpy(); tg = pose[0, :, 3].numpy().astype(np.float64)
+    assert abs(abs(np.dot(t, tg / np.linalg.norm(tg))) - 1.0) < 5e-2

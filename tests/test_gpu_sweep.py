@@ -1,0 +1,105 @@
+"""HIP plane sweep / inverse warp vs the reference's outputs (golden) and the
+oracle.  Floating-point bar (north_star): within 1e-4 relative.  Features are
+unit-variance, so the test uses |a-b| <= 1e-4*|b| + 1e-4 (1e-4 of the feature
+scale): the reference's fp32 CPU sgemm / grid_sample accumulate in a different
+order (and with FMA), which moves sample coordinates by fp32 ulps (~1e-5 px at
+311 px) and the bilinear result by ~|grad f| x 1e-5.  Observed max 3.8e-5."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import sweep as S
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 1e-4, 1e-4
+
+
+def _close(a, b):
+    a = a.float().cpu(); b = b.float().cpu()
+    err = (a - b).abs() - (RTOL * b.abs() + ATOL)
+    return float(err.max()) <= 0.0, float((a - b).abs().max())
+
+
+def test_inverse_warp_golden(golden, cuda):
+    from sfm_amd.sweep import inverse_warp
+    g = golden("warp.npz")["warp"]
+    f = torch.from_numpy(g["feat"]).to(cuda)
+    K = torch.from_numpy(g["K"]).to(cuda); Ki = torch.from_numpy(g["Kinv"]).to(cuda)
+    for k in range(g["depth"].shape[0]):
+        out = inverse_warp(f, torch.from_numpy(g["depth"][k]).to(cuda), torch.from_numpy(g["pose"][k]).to(cuda), K, Ki)
+        ok, err = _close(out, torch.from_numpy(g["out"][k]))
+        assert ok, (k, err)
+
+
+def test_cost_volume_golden(golden, cuda):
+    from sfm_amd.sweep import PlaneSweep
+    g = golden("warp.npz")["cost"]
+    ps = PlaneSweep(int(g["nlabel"]), float(g["min_depth"]), rescale_depth=True, norm_target=float(g["norm_target"]))
+    pose = torch.from_numpy(g["pose"]).unsqueeze(1).to(cuda).clone()
+    cost = ps(torch.from_numpy(g["ref"]).to(cuda), [torch.from_numpy(g["tgt"]).to(cuda)], pose,
+              torch.from_numpy(g["K"]).to(cuda), torch.from_numpy(g["Kinv"]).to(cuda))[0]
+    ref = torch.from_numpy(g["cost"])
+    C = ref.shape[1] // 2
+    assert torch.equal(cost[:, :C].cpu(), ref[:, :C])          # reference half: exact copy
+    ok, err = _close(cost[:, C:], ref[:, C:])
+    assert ok, err
+    # RESCALE_DEPTH mutates the caller's pose in place, as PSNet.forward does
+    assert torch.allclose(pose[:, 0, :, 3].cpu(), torch.from_numpy(g["pose"])[:, :, 3] * float(g["norm_target"]))
+
+
+def test_full_size_kitti_sweep(cuda):
+    """376x1242 -> 94x311 features, L=128, C=32: GPU vs oracle on a plane subset."""
+    from sfm_amd import synth
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
+    B, C, L = 2, 32, 128
+    h, w = synth.feature_hw()
+    ref, tgt = synth.features(B, C, h, w, seed=4)
+    K = synth.intrinsics(B)
+    Ki = torch.inverse(K)
+    gen = torch.Generator().manual_seed(9)
+    pose = synth.relative_pose(B, gen)
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    cost = plane_sweep_cost(ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 1.0)
+    planes = [0, 1, 5, 31, 64, 100, 127]
+    want = S.plane_sweep_cost(ref, tgt, pose, K, Ki, L, 1.0, planes=planes)
+    got = cost[:, :, planes].cpu()
+    assert torch.equal(got[:, :C], want[:, :C])
+    ok, err = _close(got[:, C:], want[:, C:])
+    assert ok, err
+    # every plane's reference half is the same copy
+    assert torch.equal(cost[:, :C, 77].cpu(), ref)
+
+
+def test_bf16_cost_volume(cuda):
+    from sfm_amd import synth
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
+    B, C, L = 1, 32, 16
+    h, w = 47, 156
+    ref, tgt = synth.features(B, C, h, w, seed=2)
+    K = synth.intrinsics(B, 180.0, 180.0, 77.0, 23.0)
+    Ki = torch.inverse(K)
+    pose = synth.relative_pose(B, torch.Generator().manual_seed(1))
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    args = (ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 1.0)
+    f32 = plane_sweep_cost(*args)
+    b16 = plane_sweep_cost(*args, dtype=torch.bfloat16)
+    assert b16.dtype == torch.bfloat16
+    assert torch.equal(b16.cpu(), f32.to(torch.bfloat16).cpu())   # RNE of the fp32 result
+
+
+def test_odd_pixel_count_and_warped_only(cuda):
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
+    from sfm_amd import synth
+    B, C, L, h, w = 3, 5, 7, 13, 21    # h*w odd -> scalar-store kernel
+    ref, tgt = synth.features(B, C, h, w, seed=5)
+    K = synth.intrinsics(B, 40.0, 42.0, 40.0, 25.0)
+    Ki = torch.inverse(K)
+    pose = synth.relative_pose(B, torch.Generator().manual_seed(2))
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    full = plane_sweep_cost(ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 0.5)
+    want = S.plane_sweep_cost(ref, tgt, pose, K, Ki, L, 0.5)
+    ok, err = _close(full, want)
+    assert ok, err
+    warped = plane_sweep_cost(None, tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 0.5, warped_only=True)
+    assert torch.equal(warped, full[:, C:])

@@ -1,0 +1,121 @@
+"""The oracle (CPU restatement) against the golden vectors generated from the
+reference's own code (oracle/gen_golden.py).  Pins the oracle before it is
+used as the checker of the HIP path."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ransac5 as R
+from oracle import sweep as S
+
+
+def test_solve5_bit_exact(golden):
+    g = golden("solve5.npz")
+    for i in range(len(g["q5"])):
+        r = R.solve5(g["q5"][i], g["qp5"][i], cheir=True)
+        assert r["nroots"] == g["nroots"][i]
+        assert r["nP"] == g["nP"][i]
+        nr = max(r["nroots"], 0)
+        assert np.array_equal(r["E_roots"][:nr].view(np.uint64), g["E_roots"][i][:nr].view(np.uint64)), i
+        k = r["nP"]
+        assert np.array_equal(r["E"][:k].view(np.uint64), g["E"][i][:k].view(np.uint64)), i
+        assert np.array_equal(r["P"][:k].view(np.uint64), g["P"][i][:k].view(np.uint64)), i
+        if k == 0 and nr > 0:   # slot 0 keeps root 0's E when nothing passes cheirality
+            assert np.array_equal(r["E"][0], g["E"][i][0])
+
+
+def test_solve5_no_cheirality(golden):
+    g = golden("solve5.npz")
+    for i in range(0, len(g["q5"]), 7):
+        r = R.solve5(g["q5"][i], g["qp5"][i], cheir=False)
+        assert r["nroots"] == g["nroots_nc"][i]
+        nr = max(r["nroots"], 0)
+        assert np.array_equal(r["E"][:nr], g["E_nc"][i][:nr])
+
+
+def test_solve5_finds_true_essential(golden):
+    """Known-answer: on exact geometric tuples one root reproduces the
+    epipolar constraint to ~1e-12 (essential_matrix_main.cu:227-233 style)."""
+    g = golden("solve5.npz")
+    for i in range(600, 800):
+        r = R.solve5(g["q5"][i], g["qp5"][i], cheir=False)
+        assert r["nroots"] >= 1
+        q = np.c_[g["q5"][i], np.ones(5)]
+        qp = np.c_[g["qp5"][i], np.ones(5)]
+        for E in r["E"][: r["nroots"]]:
+            E = E.reshape(3, 3)
+            res = np.abs(np.einsum("ni,ij,nj->n", qp, E, q)).max() / np.abs(E).max()
+            assert res < 1e-8
+
+
+@pytest.mark.parametrize("case", ["dense_tr_equal", "harness_style", "no_cheirality", "tight_threshold",
+                                  "test_gt_ransac", "tiny_n"])
+def test_ransac_matches_reference(golden, case):
+    g = golden("ransac.npz")[case]
+    n, nt, nr, it, thr, cheir, seed = g["params"]
+    r = R.ransac5(g["q"], g["qp"], int(nt), int(nr), int(it), float(thr), seed=int(seed), cheir=bool(cheir))
+    assert r["winner"] == int(g["winner"])
+    assert r["inliers"] == int(g["inliers"])
+    assert np.array_equal(r["E"], g["E"])
+    assert np.array_equal(r["P"], g["P"])
+    assert np.array_equal(r["hyp_score"], g["hyp_score"])
+    assert np.array_equal(r["hyp_ncand"], g["hyp_ncand"])
+    m = R.inlier_mask(r["E"], g["q"], g["qp"], float(thr))
+    assert np.array_equal(m, g["mask"])
+    assert int(m[: int(nr)].sum()) == r["inliers"]
+
+
+def test_sampler_golden(golden):
+    g = golden("sampler.npz")
+    for a, s in enumerate(g["seeds"]):
+        for b, h in enumerate(g["hs"]):
+            for d in range(5):
+                assert R.philox_u32(int(s), int(h), d) == g["u32"][a, b, d]
+                for c, n in enumerate(g["ns"]):
+                    assert R.sample_index(int(s), int(h), d, int(n)) == g["idx"][a, b, d, c]
+
+
+def test_sampler_range_and_spread():
+    n = 435032
+    idx = np.array([R.sample_index(1234, h, d, n) for h in range(2000) for d in range(5)])
+    assert idx.min() >= 0 and idx.max() <= n - 1
+    # roughly uniform: each decile populated
+    hist = np.histogram(idx, bins=10, range=(0, n))[0]
+    assert hist.min() > 0.07 * len(idx)
+
+
+def test_irls_and_decompose(golden):
+    g = golden("irls.npz")
+    for k, c in g.items():
+        assert np.array_equal(R.optimise(c["q"], c["qp"], c["E_init"], 0.001, 0.0, 200), c["E_opt"]), k
+        assert np.array_equal(R.optimise(c["q"], c["qp"], c["E_init"], 0.002, 1.0, 20), c["E_opt_huber"]), k
+        assert np.array_equal(R.decompose(c["E_init"]), c["params"])
+        U, V = R.decompose_uv(c["E_init"])
+        assert np.array_equal(U, c["U"]) and np.array_equal(V, c["V"])
+        # E = U diag(1,1,0) V^T up to scale
+        E = c["E_init"] / np.linalg.norm(c["E_init"]) * np.sqrt(2)
+        rec = U @ np.diag([1.0, 1.0, 0.0]) @ V.T
+        assert min(np.abs(rec - E).max(), np.abs(rec + E).max()) < 1e-9
+
+
+def test_inverse_warp_oracle(golden):
+    g = golden("warp.npz")["warp"]
+    K = torch.from_numpy(g["K"]); Ki = torch.from_numpy(g["Kinv"]); f = torch.from_numpy(g["feat"])
+    for k in range(g["depth"].shape[0]):
+        out = S.inverse_warp(f, torch.from_numpy(g["depth"][k]), torch.from_numpy(g["pose"][k]), K, Ki)
+        assert torch.equal(out, torch.from_numpy(g["out"][k]))
+
+
+def test_cost_volume_oracle(golden):
+    g = golden("warp.npz")["cost"]
+    cost = S.plane_sweep_cost(torch.from_numpy(g["ref"]), torch.from_numpy(g["tgt"]), torch.from_numpy(g["pose"]),
+                              torch.from_numpy(g["K"]), torch.from_numpy(g["Kinv"]), int(g["nlabel"]),
+                              float(g["min_depth"]), rescale=float(g["norm_target"]))
+    assert torch.equal(cost, torch.from_numpy(g["cost"]))
+
+
+def test_flow2depth_oracle(golden):
+    g = golden("warp.npz")["flow2depth"]
+    out = S.flow2depth(torch.from_numpy(g["R"]), torch.from_numpy(g["T"]), torch.zeros(*g["shape"].tolist()),
+                       torch.from_numpy(g["K"]))
+    assert torch.allclose(out, torch.from_numpy(g["out"]), rtol=0, atol=1e-5)
