@@ -18,10 +18,11 @@
 //   k_select  per pair: preselect/rescore per hypothesis, first-max argmax.
 //
 // Inlier decisions are bit-identical to the reference's IEEE evaluation
-// |x'^T E x| / sqrt(Ex0^2+Ex1^2+xE0^2+xE1^2) <= thr: the products and sums are
-// evaluated in the reference's order without contraction, and the
-// sqrt+division is replaced by a squared comparison with a 2^-40 relative
-// guard band; the (rare) values inside the band take the exact IEEE path.
+// e = |x'^T E x| / sqrt(Ex0^2+Ex1^2+xE0^2+xE1^2) <= thr (ComputeError,
+// kernel_functions.cu:232-264).  The score kernel decides most (candidate,
+// point) pairs on an FMA evaluation with a proven error bound (see
+// inlier_fast below) and re-evaluates the rare undecided ones in the
+// reference's exact operation order.
 #include <algorithm>
 #include <vector>
 #include "common.h"
@@ -33,12 +34,11 @@ constexpr int kChains = SFM_RANSAC_CHAINS;
 constexpr int kMaxSlots = 10;
 constexpr int kCandStride = 12;   // doubles per candidate E (9 used), 96 B
 constexpr int kKC = 32;           // candidates per score tile
-constexpr int kPPL = 4;           // points per lane per chunk
+constexpr int kPPL = 8;           // points per lane per chunk
 constexpr int kScoreThreads = 256;
 constexpr int kChunk = kScoreThreads * kPPL;
-constexpr int kChunksPerItem = 8;
+constexpr int kChunksPerItem = 4;
 constexpr int kPtsPerItem = kChunk * kChunksPerItem;   // 8192
-constexpr double kDmin = 0x1p-900;
 
 struct PairParams {
   int64_t n[SFM_MAX_BATCH];
@@ -151,6 +151,32 @@ __global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, in
 }
 
 // ---------------------------------------------------------------------------
+// Fast inlier decision: error bound (derivation in DESIGN.md, "Scoring").
+//
+// With u = 2^-53, R = sum |E_ij| and M = max(1, |x|, |y|, |x'|, |y'|), the
+// FMA-evaluated quantities used below differ from the values the reference's
+// operation order produces by at most
+//     |a_f - a_r| <= 11 u M^2 R,   ||v_f - v_r|| <= 10.0002 u R M
+// (v = (Ex0, Ex1, xE0, xE1), a = x'^T E x, D = ||v||^2).  Deciding
+//     inlier  if a_f^2 < thr^2 (1 - 2^-22) D_f,
+//     outlier if a_f^2 > thr^2 (1 + 2^-22) D_f
+// is then provably identical to the reference's IEEE test whenever
+//     D_f >= (u R M^2 G)^2,   G = 2^24 (11 + 11/thr),
+// and 2^-40 <= thr < 1, 2^-100 <= R <= 2^100, M <= 2^100.  Every other
+// (candidate, point) pair takes the exact path.  Per candidate the constant
+// Kg = (u R G)^2 is stored in candE[9] (NaN disables the fast path); per
+// point mm2 = M^4, so the guard is D_f >= Kg * mm2.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double guard_constant(const double* E, double g) {
+  double R = 0.0;
+#pragma unroll
+  for (int e = 0; e < 9; ++e) R += fabs(E[e]);
+  if (!(R >= 0x1p-100 && R <= 0x1p100) || !(g > 0.0)) return __builtin_nan("");
+  const double k = 0x1p-53 * R * g;
+  return k * k;
+}
+
+// ---------------------------------------------------------------------------
 // Phase 2: chains and the dense candidate list (one block of 512 per pair)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
@@ -161,7 +187,7 @@ __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
                                                    double* __restrict__ hypP0,
                                                    int32_t* __restrict__ cand_off,
                                                    int32_t* __restrict__ cand_total,
-                                                   double* __restrict__ candE, int cmax) {
+                                                   double* __restrict__ candE, int cmax, double guard_g) {
   __shared__ int32_t s_sum[kChains / 64];
   const int b = blockIdx.x, t = threadIdx.x;
   const size_t hb0 = (size_t)b * H;
@@ -198,14 +224,19 @@ __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
     const double* Eh = hypE + hb * kMaxSlots * 9;
     cand_off[hb] = off;
     if (nc > 0) {
-      for (int j = 0; j < nc; ++j)
+      for (int j = 0; j < nc; ++j) {
+        double* dst = cE + (size_t)(off + j) * kCandStride;
 #pragma unroll
-        for (int e = 0; e < 9; ++e) cE[(size_t)(off + j) * kCandStride + e] = Eh[j * 9 + e];
+        for (int e = 0; e < 9; ++e) dst[e] = Eh[j * 9 + e];
+        dst[9] = guard_constant(dst, guard_g);
+      }
       off += nc;
     } else {
       // rescore-only candidate: slot 0 as the reference thread would hold it
+      double* dst = cE + (size_t)off * kCandStride;
 #pragma unroll
-      for (int e = 0; e < 9; ++e) cE[(size_t)off * kCandStride + e] = nr > 0 ? Eh[e] : E0[e];
+      for (int e = 0; e < 9; ++e) dst[e] = nr > 0 ? Eh[e] : E0[e];
+      dst[9] = guard_constant(dst, guard_g);
 #pragma unroll
       for (int e = 0; e < 12; ++e) hypP0[hb * 12 + e] = P0[e];
       off += 1;
@@ -236,9 +267,9 @@ __device__ __forceinline__ bool inlier_exact(double a, double D, double thr) {
   return e <= thr;
 }
 
-template <bool FAST>
-__device__ __forceinline__ bool inlier_test(const double* E, double x, double y, double xp, double yp,
-                                            const ScoreConsts& k) {
+// Reference operation order, no contraction (ComputeError).
+__device__ __forceinline__ bool inlier_reference(const double* E, double x, double y, double xp, double yp,
+                                                 double thr) {
   const double ex0 = (E[0] * x + E[1] * y) + E[2];
   const double ex1 = (E[3] * x + E[4] * y) + E[5];
   const double ex2 = (E[6] * x + E[7] * y) + E[8];
@@ -246,13 +277,46 @@ __device__ __forceinline__ bool inlier_test(const double* E, double x, double y,
   const double xe1 = (xp * E[1] + yp * E[4]) + E[7];
   const double a = (xp * ex0 + yp * ex1) + ex2;
   const double D = ((ex0 * ex0 + ex1 * ex1) + xe0 * xe0) + xe1 * xe1;
-  if (!FAST) return inlier_exact(a, D, k.thr);
+  return inlier_exact(a, D, thr);
+}
+
+// mm2 = M^4 for the fast-path guard (NaN for non-finite / huge coordinates)
+__device__ __forceinline__ double point_scale(double x, double y, double xp, double yp) {
+  double M = fmax(fmax(fabs(x), fabs(y)), fmax(fabs(xp), fabs(yp)));
+  M = fmax(M, 1.0);
+  if (!(M <= 0x1p100)) return __builtin_nan("");
+  const double M2 = M * M;
+  return M2 * M2;
+}
+
+// Wave-uniform value copied into a VGPR: one VALU op may read only one SGPR,
+// so the FMA-chain addends are broadcast once per candidate instead of being
+// re-materialised for every point.
+__device__ __forceinline__ double to_vgpr(double s) {
+  double v;
+  asm("v_mov_b64 %0, %1" : "=v"(v) : "s"(s));
+  return v;
+}
+
+struct Addends { double e2, e5, e8, e6, e7; };
+
+template <bool FAST>
+__device__ __forceinline__ bool inlier_test(const double* E, const Addends& ad, double Kg, double x, double y,
+                                            double xp, double yp, double mm2, const ScoreConsts& k) {
+  if (!FAST) return inlier_reference(E, x, y, xp, yp, k.thr);
+  const double ex0 = fma(E[0], x, fma(E[1], y, ad.e2));
+  const double ex1 = fma(E[3], x, fma(E[4], y, ad.e5));
+  const double ex2 = fma(E[6], x, fma(E[7], y, ad.e8));
+  const double xe0 = fma(xp, E[0], fma(yp, E[3], ad.e6));
+  const double xe1 = fma(xp, E[1], fma(yp, E[4], ad.e7));
+  const double a = fma(xp, ex0, fma(yp, ex1, ex2));
+  const double D = fma(xe1, xe1, fma(xe0, xe0, fma(ex1, ex1, ex0 * ex0)));
   const double lhs = a * a;
-  const bool g = D >= kDmin;
+  const bool g = D >= Kg * mm2;
   const bool fin = g && (lhs < k.t2lo * D);
   const bool fout = g && (lhs > k.t2hi * D);
   bool in = fin;
-  if (!(fin || fout)) in = inlier_exact(a, D, k.thr);
+  if (!(fin || fout)) in = inlier_reference(E, x, y, xp, yp, k.thr);
   return in;
 }
 
@@ -296,7 +360,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restric
     const double* P = pts + (size_t)b * n_stride * 4;
     const double* CE = candE + ((size_t)b * cmax + c0) * kCandStride;
     for (int cb = p0; cb < p1; cb += kChunk) {
-      double x[kPPL], y[kPPL], xp[kPPL], yp[kPPL];
+      double x[kPPL], y[kPPL], xp[kPPL], yp[kPPL], mm2[kPPL];
       bool vT[kPPL], vR[kPPL];
 #pragma unroll
       for (int k = 0; k < kPPL; ++k) {
@@ -304,6 +368,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restric
         const bool ok = p < p1;
         const double4 v = *reinterpret_cast<const double4*>(P + (size_t)(ok ? p : p0) * 4);
         x[k] = v.x; y[k] = v.y; xp[k] = v.z; yp[k] = v.w;
+        mm2[k] = point_scale(v.x, v.y, v.z, v.w);
         vT[k] = ok && p < T;
         vR[k] = ok && p < R;
       }
@@ -311,10 +376,13 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restric
         double E[9];
 #pragma unroll
         for (int e = 0; e < 9; ++e) E[e] = CE[(size_t)c * kCandStride + e];
+        const double Kg = CE[(size_t)c * kCandStride + 9];
+        Addends ad;
+        if (FAST) ad = Addends{to_vgpr(E[2]), to_vgpr(E[5]), to_vgpr(E[8]), to_vgpr(E[6]), to_vgpr(E[7])};
         int sT = 0, sR = 0;
 #pragma unroll
         for (int k = 0; k < kPPL; ++k) {
-          const bool in = inlier_test<FAST>(E, x[k], y[k], xp[k], yp[k], kc);
+          const bool in = inlier_test<FAST>(E, ad, Kg, x[k], y[k], xp[k], yp[k], mm2[k], kc);
           sT += __popcll(__ballot(in && vT[k]));
           sR += __popcll(__ballot(in && vR[k]));
         }
@@ -415,8 +483,7 @@ __global__ void k_inlier_mask(const double* __restrict__ pts, int64_t n_stride, 
   uint8_t m = 0;
   if (k < pp.n[b]) {
     const double4 v = *reinterpret_cast<const double4*>(pts + ((size_t)b * n_stride + k) * 4);
-    const ScoreConsts kc{thr, 0.0, 0.0};
-    m = inlier_test<false>(E + (size_t)b * 9, v.x, v.y, v.z, v.w, kc) ? 1 : 0;
+    m = inlier_reference(E + (size_t)b * 9, v.x, v.y, v.z, v.w, thr) ? 1 : 0;
   }
   mask[(size_t)b * n_stride + k] = m;
 }
@@ -473,16 +540,17 @@ static int run_chunk(const double* pts, int64_t n_stride, const int64_t* n, int 
                        w.nroots, w.ncand, w.hypE, w.hypP);
   }
   SFM_LAUNCHED();
+  const bool fast = thr >= 0x1p-40 && thr < 1.0;
+  const double guard_g = fast ? 0x1p24 * (11.0 + 11.0 / thr) : 0.0;
   {
     ProfScope ps("ransac_chain", s);
     hipLaunchKernelGGL(k_chain, dim3(bc), dim3(kChains), 0, s, H, iters, cheir, w.nroots, w.ncand, w.hypE,
-                       w.hypP, w.hypP0, w.cand_off, w.cand_total, w.candE, cmax);
+                       w.hypP, w.hypP0, w.cand_off, w.cand_total, w.candE, cmax, guard_g);
   }
   SFM_LAUNCHED();
   SFM_HIP(hipMemsetAsync(w.cntT, 0, (size_t)bc * cmax * 4, s));
   SFM_HIP(hipMemsetAsync(w.cntR, 0, (size_t)bc * cmax * 4, s));
-  const bool fast = thr >= 0x1p-40 && thr < 1.0;
-  ScoreConsts kc{thr, (thr * thr) * (1.0 - 0x1p-40), (thr * thr) * (1.0 + 0x1p-40)};
+  ScoreConsts kc{thr, (thr * thr) * (1.0 - 0x1p-22), (thr * thr) * (1.0 + 0x1p-22)};
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = std::max(1, cus) * 8;

@@ -2,15 +2,8 @@
 //
 // Replaces the per-plane Python loop of models/PSNet.py:144-158 (L iterations
 // of ~10 ATen launches: bmm, elementwise, grid_sample, two strided copies)
-// with one launch that writes the whole [B, 2C, L, h, w] volume.  Each thread
-// owns PIX consecutive pixels of one pair and a run of planes: the
-// plane-independent ray K4^-1 (x, y, 1) and the C reference-feature values are
-// computed / loaded once and reused across the planes; per plane the warp
-// (inverse_warp.py:121-153) gives 4 bilinear taps gathered from the CHW target
-// features (neighbouring lanes sample neighbouring source pixels, so each
-// gather instruction touches one or two cache lines), and 2C output rows are
-// written with PIX-wide vector stores (non-temporal: the volume is written
-// once and consumed by a later kernel).  HBM-write-bound.
+// with one launch that writes the whole [B, 2C, L, h, w] volume (plus a tiny
+// channel-quad relayout of the target features).  HBM-write-bound.
 //
 // Arithmetic follows the reference's float32 expression order:
 //   cam = (Kinv . (x, y, 1)) * d              pixel2cam (27-41)
@@ -19,12 +12,12 @@
 //   grid_sample bilinear, zeros padding, align_corners=True
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <string>
 #include "common.h"
 
 namespace sfm {
 
 constexpr int kSweepThreads = 256;
-constexpr int kPlanesPerBlock = 16;
 
 struct Proj {   // (K . pose) rows and Kinv
   float m[12];
@@ -92,114 +85,154 @@ __device__ __forceinline__ unsigned short to_bf16(float f) {
   return *reinterpret_cast<unsigned short*>(&b);
 }
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+// ---------------------------------------------------------------------------
+// Cost volume, v2: the output is produced in address order.
+//
+// Work item = (pair b, 4-row channel group g, plane l, 1024-pixel window):
+// 256 threads x 4 consecutive pixels write four 4 KB row segments with
+// 16-byte stores.  Items are enumerated with the window fastest, then the
+// plane, then the group, then the pair, and each block takes kSwItems
+// consecutive items, so the chip streams through the [B, 2C, L, h, w] volume
+// roughly in address order (a volume written as thousands of scattered row
+// chunks tops out ~20% lower on MI355X: scripts/probe_store_bw.hip).
+//
+// Groups [0, C4) copy the reference features (rows c < C, identical for every
+// plane); groups [C4, 2 C4) are the warped target features: the 4 bilinear
+// taps of each pixel are read as float4 from the channel-quad layout
+// tq[B][C4][h*w][4] (one 16-byte load per tap per 4 channels).
+//
+// 16-byte alignment: a row starts at element ((b*rows + r)*L + l)*h*w.  With
+// h*w = 2 (mod 4) and L even, that is 2*(l & 1) (mod 4) for every row of the
+// plane, so the pixel windows of odd planes are shifted by 2.  Other shapes
+// take the element-wise store path (correct, slower).
+// ---------------------------------------------------------------------------
+constexpr int kSwThreads = 256;
+constexpr int kSwPix = 4;
+constexpr int kSwWin = kSwThreads * kSwPix;
+constexpr int kSwItems = 8;
 
-template <int PIX>
-__device__ __forceinline__ void store_px(float* dst, const float (&v)[PIX]) {
-  if constexpr (PIX == 2) {
-    f32x2 pv = {v[0], v[1]};
-    __builtin_nontemporal_store(pv, reinterpret_cast<f32x2*>(dst));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// tgt [B][C][hw] -> tq [B][C4][hw] float4 (channels >= C are zero)
+__global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4, int hw, f32x4* __restrict__ tq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)B * C4 * hw;
+  if (i >= total) return;
+  const int p = (int)(i % hw);
+  const int64_t bq = i / hw;
+  const int q = (int)(bq % C4), b = (int)(bq / C4);
+  f32x4 v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = 4 * q + k;
+    v[k] = c < C ? tgt[((size_t)b * C + c) * hw + p] : 0.0f;
+  }
+  tq[i] = v;
+}
+
+__device__ __forceinline__ void store4(float* dst, const float (&v)[4]) {
+  *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ void store4(unsigned short* dst, const float (&v)[4]) {
+  u32x2 u;
+  u[0] = (unsigned int)to_bf16(v[0]) | ((unsigned int)to_bf16(v[1]) << 16);
+  u[1] = (unsigned int)to_bf16(v[2]) | ((unsigned int)to_bf16(v[3]) << 16);
+  *reinterpret_cast<u32x2*>(dst) = u;
+}
+__device__ __forceinline__ void store1(float* dst, float v) { *dst = v; }
+__device__ __forceinline__ void store1(unsigned short* dst, float v) { *dst = to_bf16(v); }
+
+// VEC: rows are 16-byte aligned at the (shifted) window starts (see above)
+template <typename OutT, bool VEC>
+__device__ __forceinline__ void store_row(OutT* row, int p0, int hw, const float (&v)[4]) {
+  if (VEC && p0 >= 0 && p0 + 3 < hw) {
+    store4(row + p0, v);
   } else {
-    __builtin_nontemporal_store(v[0], dst);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (p0 + j >= 0 && p0 + j < hw) store1(row + p0 + j, v[j]);
   }
 }
-template <int PIX>
-__device__ __forceinline__ void store_px(unsigned short* dst, const float (&v)[PIX]) {
-  if constexpr (PIX == 2) {
-    const unsigned int u = (unsigned int)to_bf16(v[0]) | ((unsigned int)to_bf16(v[1]) << 16);
-    __builtin_nontemporal_store(u, reinterpret_cast<unsigned int*>(dst));
-  } else {
-    __builtin_nontemporal_store(to_bf16(v[0]), dst);
-  }
-}
 
-// One thread: PIX consecutive flat pixels x kPlanesPerBlock planes of pair b.
-// WITH_REF: also write the reference half (channels [0, C)).
-template <typename OutT, int PIX, bool WITH_REF>
-__global__ __launch_bounds__(kSweepThreads) void k_plane_sweep(const float* __restrict__ ref,
-                                                               const float* __restrict__ tgt, int batch, int C,
-                                                               int h, int w, const float* __restrict__ pose,
-                                                               const float* __restrict__ K4,
-                                                               const float* __restrict__ K4inv, int L,
-                                                               float dmax, OutT* __restrict__ out) {
+template <typename OutT, bool VEC>
+__global__ __launch_bounds__(kSwThreads) void k_sweep(const float* __restrict__ ref, const f32x4* __restrict__ tq,
+                                                      int B, int C, int C4, int h, int w,
+                                                      const float* __restrict__ pose, const float* __restrict__ K4,
+                                                      const float* __restrict__ K4inv, int L, float dmax,
+                                                      int with_ref, int shift_mode, OutT* __restrict__ out) {
   const int hw = h * w;
-  const int pix_blocks = (hw + kSweepThreads * PIX - 1) / (kSweepThreads * PIX);
-  const int plane_groups = (L + kPlanesPerBlock - 1) / kPlanesPerBlock;
-  // pair is the fastest-varying block coordinate: with round-robin XCD
-  // dispatch a pair's blocks share one XCD's L2 when batch divides 8.
-  int bid = blockIdx.x;
-  const int b = bid % batch;
-  bid /= batch;
-  const int pg = bid % plane_groups;
-  const int pb = bid / plane_groups;
-  if (pb >= pix_blocks) return;
-  const int p0 = (pb * kSweepThreads + threadIdx.x) * PIX;
-  if (p0 >= hw) return;
-  const int np = min(PIX, hw - p0);
-
-  Proj pr;
-  load_proj(pose, K4, K4inv, b, pr);
-  float ray[PIX][3];
+  const int npw = (hw + 3 + kSwWin - 1) / kSwWin;
+  const int groups = with_ref ? 2 * C4 : C4;
+  const int rows = with_ref ? 2 * C : C;
+  const int64_t per_group = (int64_t)L * npw;
+  const int64_t total = (int64_t)B * groups * per_group;
+  const int64_t first = (int64_t)blockIdx.x * kSwItems;
+  for (int it = 0; it < kSwItems; ++it) {
+    const int64_t item = first + it;
+    if (item >= total) return;
+    const int pw = (int)(item % npw);
+    int64_t r = item / npw;
+    const int l = (int)(r % L);
+    r /= L;
+    const int g = (int)(r % groups);
+    const int b = (int)(r / groups);
+    const int shift = shift_mode ? 2 * (l & 1) : 0;
+    const int p0 = pw * kSwWin - shift + threadIdx.x * kSwPix;
+    if (p0 >= hw) continue;
+    OutT* plane = out + ((size_t)b * rows * L + l) * hw;    // row r at plane + r * L * hw
+    const size_t rstride = (size_t)L * hw;
+    if (with_ref && g < C4) {
+      // reference half: rows 4g .. 4g+3
+      const float* R = ref + (size_t)b * C * hw;
 #pragma unroll
-  for (int k = 0; k < PIX; ++k) {
-    const int p = min(p0 + k, hw - 1);
-    const float x = (float)(p % w), y = (float)(p / w);
-    ray[k][0] = (pr.ki[0] * x + pr.ki[1] * y) + pr.ki[2];
-    ray[k][1] = (pr.ki[3] * x + pr.ki[4] * y) + pr.ki[5];
-    ray[k][2] = (pr.ki[6] * x + pr.ki[7] * y) + pr.ki[8];
-  }
-  const float* T = tgt + (size_t)b * C * hw;
-  const float* Rf = ref + (size_t)b * C * hw;
-  const int cout = WITH_REF ? 2 * C : C;
-  const int cbase = WITH_REF ? C : 0;
-  const size_t plane_stride = (size_t)hw;            // between planes of one channel
-  const size_t chan_stride = (size_t)L * hw;         // between channels
-  OutT* O = out + (size_t)b * cout * chan_stride + p0;
-  const int l0 = pg * kPlanesPerBlock, l1 = min(L, l0 + kPlanesPerBlock);
-  const bool full = np == PIX;
-
-  for (int l = l0; l < l1; ++l) {
-    const float d = dmax / (float)(l + 1);
-    Taps tp[PIX];
-    bool ok[PIX];
+      for (int k = 0; k < 4; ++k) {
+        const int c = 4 * g + k;
+        if (c >= C) break;
+        float v[4];
 #pragma unroll
-    for (int k = 0; k < PIX; ++k) {
-      float ix, iy;
-      ok[k] = sample_pos(pr, ray[k], d, h, w, ix, iy);
-      if (ok[k]) make_taps(ix, iy, h, w, tp[k]);
-      else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { tp[k].off[j] = 0; tp[k].wt[j] = 0.0f; }
-      }
-    }
-    OutT* Ol = O + (size_t)l * plane_stride;
-    if (WITH_REF) {
-      for (int c = 0; c < C; ++c) {
-        float v[PIX];
-#pragma unroll
-        for (int k = 0; k < PIX; ++k) v[k] = Rf[(size_t)c * hw + min(p0 + k, hw - 1)];
-        OutT* dst = Ol + (size_t)c * chan_stride;
-        if (full) store_px<PIX>(dst, v);
-        else for (int k = 0; k < np; ++k) { float s[1] = {v[k]}; store_px<1>(dst + k, s); }
-      }
-    }
-    for (int c = 0; c < C; ++c) {
-      const float* Tc = T + (size_t)c * hw;
-      float v[PIX];
-#pragma unroll
-      for (int k = 0; k < PIX; ++k) {
-        float acc = 0.0f;
-        if (ok[k]) {
-          acc = tp[k].wt[0] * Tc[tp[k].off[0]];
-          acc = acc + tp[k].wt[1] * Tc[tp[k].off[1]];
-          acc = acc + tp[k].wt[2] * Tc[tp[k].off[2]];
-          acc = acc + tp[k].wt[3] * Tc[tp[k].off[3]];
+        for (int j = 0; j < 4; ++j) {
+          const int p = min(max(p0 + j, 0), hw - 1);
+          v[j] = R[(size_t)c * hw + p];
         }
-        v[k] = acc;
+        store_row<OutT, VEC>(plane + (size_t)c * rstride, p0, hw, v);
       }
-      OutT* dst = Ol + (size_t)(cbase + c) * chan_stride;
-      if (full) store_px<PIX>(dst, v);
-      else for (int k = 0; k < np; ++k) { float s[1] = {v[k]}; store_px<1>(dst + k, s); }
+      continue;
+    }
+    const int q = with_ref ? g - C4 : g;
+    Proj pr;
+    load_proj(pose, K4, K4inv, b, pr);
+    const float d = dmax / (float)(l + 1);
+    const f32x4* T = tq + ((size_t)b * C4 + q) * hw;
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = min(max(p0 + j, 0), hw - 1);
+      const float x = (float)(p % w), y = (float)(p / w);
+      float ray[3];
+      ray[0] = (pr.ki[0] * x + pr.ki[1] * y) + pr.ki[2];
+      ray[1] = (pr.ki[3] * x + pr.ki[4] * y) + pr.ki[5];
+      ray[2] = (pr.ki[6] * x + pr.ki[7] * y) + pr.ki[8];
+      float ix, iy;
+      acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (sample_pos(pr, ray, d, h, w, ix, iy)) {
+        Taps tp;
+        make_taps(ix, iy, h, w, tp);
+        const f32x4 t0 = T[tp.off[0]], t1 = T[tp.off[1]], t2 = T[tp.off[2]], t3 = T[tp.off[3]];
+        f32x4 a = tp.wt[0] * t0;
+        a = a + tp.wt[1] * t1;
+        a = a + tp.wt[2] * t2;
+        a = a + tp.wt[3] * t3;
+        acc[j] = a;
+      }
+    }
+    const int cbase = with_ref ? C : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * q + k;
+      if (c >= C) break;
+      const float v[4] = {acc[0][k], acc[1][k], acc[2][k], acc[3][k]};
+      store_row<OutT, VEC>(plane + (size_t)(cbase + c) * rstride, p0, hw, v);
     }
   }
 }
@@ -241,29 +274,47 @@ __global__ __launch_bounds__(kSweepThreads) void k_inverse_warp(const float* __r
   }
 }
 
-template <bool WITH_REF>
-static int launch_sweep(const float* ref, const float* tgt, int batch, int C, int h, int w, const float* pose,
-                        const float* K4, const float* K4inv, int L, float min_depth, int out_dtype, void* out,
-                        hipStream_t s) {
-  SFM_REQUIRE(tgt && pose && K4 && K4inv && out && (!WITH_REF || ref), "null pointer argument");
-  SFM_REQUIRE(batch >= 1 && C >= 1 && h >= 2 && w >= 2 && L >= 1, "invalid sweep shape");
+static size_t sweep_ws_bytes(int B, int C, int h, int w) {
+  const int C4 = (C + 3) / 4;
+  return (size_t)B * C4 * (size_t)h * w * 16;
+}
+
+static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B, int C, int h, int w,
+                        const float* pose, const float* K4, const float* K4inv, int L, float min_depth,
+                        int out_dtype, void* out, void* ws, size_t ws_bytes, hipStream_t s) {
+  SFM_REQUIRE(tgt && pose && K4 && K4inv && out && (!with_ref || ref), "null pointer argument");
+  SFM_REQUIRE(B >= 1 && C >= 1 && h >= 2 && w >= 2 && L >= 1, "invalid sweep shape");
   SFM_REQUIRE(out_dtype == 0 || out_dtype == 1, "out_dtype must be 0 (float32) or 1 (bfloat16)");
-  SFM_REQUIRE((int64_t)h * w < (int64_t)1 << 31, "feature map too large");
-  const int hw = h * w;
-  const bool even = (hw % 2) == 0;
-  const int pix = even ? 2 : 1;
-  const int pix_blocks = (hw + kSweepThreads * pix - 1) / (kSweepThreads * pix);
-  const int plane_groups = (L + kPlanesPerBlock - 1) / kPlanesPerBlock;
-  const int64_t blocks = (int64_t)pix_blocks * plane_groups * batch;
-  SFM_REQUIRE(blocks < (int64_t)1 << 31, "sweep grid too large");
-  // planes d_i = (MIN_DEPTH * L) / (i + 1): disp2depth = ones * mindepth * nlabel (fp32)
-  const float dmax = min_depth * (float)L;
-  ProfScope ps(WITH_REF ? "plane_sweep" : "plane_sweep_warped", s);
-#define SFM_SWEEP_LAUNCH(OT, P)                                                                          \
-  hipLaunchKernelGGL((k_plane_sweep<OT, P, WITH_REF>), dim3((unsigned)blocks), dim3(kSweepThreads), 0, s, \
-                     ref, tgt, batch, C, h, w, pose, K4, K4inv, L, dmax, (OT*)out)
-  if (out_dtype == 0) { if (even) SFM_SWEEP_LAUNCH(float, 2); else SFM_SWEEP_LAUNCH(float, 1); }
-  else { if (even) SFM_SWEEP_LAUNCH(unsigned short, 2); else SFM_SWEEP_LAUNCH(unsigned short, 1); }
+  SFM_REQUIRE((int64_t)h * w < ((int64_t)1 << 30), "feature map too large");
+  const size_t need = sweep_ws_bytes(B, C, h, w);
+  if (!ws || ws_bytes < need) {
+    set_error("plane sweep workspace too small: need " + std::to_string(need) + " bytes");
+    return SFM_ERR_WORKSPACE;
+  }
+  const int hw = h * w, C4 = (C + 3) / 4;
+  const int npw = (hw + 3 + kSwWin - 1) / kSwWin;
+  const int groups = with_ref ? 2 * C4 : C4;
+  const int64_t items = (int64_t)B * groups * L * npw;
+  const int64_t blocks = (items + kSwItems - 1) / kSwItems;
+  SFM_REQUIRE(blocks < ((int64_t)1 << 31), "sweep grid too large");
+  // 16-byte row alignment (see k_sweep): every row aligned if hw % 4 == 0; rows of
+  // plane l shifted by 2*(l&1) if hw % 4 == 2 and L even; element stores otherwise
+  const bool vec = (hw % 4 == 0) || (hw % 4 == 2 && L % 2 == 0);
+  const int shift_mode = (hw % 4 == 2 && L % 2 == 0) ? 1 : 0;
+  const float dmax = min_depth * (float)L;   // disp2depth = ones * MIN_DEPTH * nlabel (fp32)
+  f32x4* tq = (f32x4*)ws;
+  {
+    ProfScope ps("sweep_tgt_quads", s);
+    const int64_t n = (int64_t)B * C4 * hw;
+    hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tgt, B, C, C4, hw, tq);
+  }
+  SFM_LAUNCHED();
+  ProfScope ps(with_ref ? "plane_sweep" : "plane_sweep_warped", s);
+#define SFM_SWEEP_LAUNCH(OT, V)                                                                              \
+  hipLaunchKernelGGL((k_sweep<OT, V>), dim3((unsigned)blocks), dim3(kSwThreads), 0, s, ref, tq, B, C, C4, h, w, \
+                     pose, K4, K4inv, L, dmax, with_ref ? 1 : 0, shift_mode, (OT*)out)
+  if (out_dtype == 0) { if (vec) SFM_SWEEP_LAUNCH(float, true); else SFM_SWEEP_LAUNCH(float, false); }
+  else { if (vec) SFM_SWEEP_LAUNCH(unsigned short, true); else SFM_SWEEP_LAUNCH(unsigned short, false); }
 #undef SFM_SWEEP_LAUNCH
   SFM_LAUNCHED();
   return SFM_OK;
@@ -275,18 +326,23 @@ using namespace sfm;
 
 extern "C" {
 
+size_t sfm_plane_sweep_workspace_bytes(int batch, int channels, int h, int w) {
+  if (batch < 1 || channels < 1 || h < 1 || w < 1) return 0;
+  return sweep_ws_bytes(batch, channels, h, w);
+}
+
 int sfm_plane_sweep(const float* ref, const float* tgt, int batch, int channels, int h, int w, const float* pose,
                     const float* K4, const float* K4inv, int nlabel, float min_depth, int out_dtype, void* cost,
-                    void* stream) {
-  return launch_sweep<true>(ref, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, out_dtype, cost,
-                            (hipStream_t)stream);
+                    void* workspace, size_t workspace_bytes, void* stream) {
+  return launch_sweep(true, ref, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, out_dtype, cost,
+                      workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w, const float* pose,
                            const float* K4, const float* K4inv, int nlabel, float min_depth, int out_dtype,
-                           void* out, void* stream) {
-  return launch_sweep<false>(nullptr, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, out_dtype,
-                             out, (hipStream_t)stream);
+                           void* out, void* workspace, size_t workspace_bytes, void* stream) {
+  return launch_sweep(false, nullptr, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, out_dtype,
+                      out, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int sfm_inverse_warp(const float* feat, int batch, int channels, int h, int w, const float* depth,

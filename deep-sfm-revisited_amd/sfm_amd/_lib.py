@@ -37,12 +37,13 @@ _SIGS = [
      [_c_dp, _c_dp, ctypes.c_int64, _c_dp, ctypes.c_double, ctypes.c_double, ctypes.c_int, _c_dp]),
     ("sfm_essential_decompose", ctypes.c_int, [_c_dp, _c_dp]),
     ("sfm_essential_decompose_uv", ctypes.c_int, [_c_dp, _c_dp, _c_dp]),
+    ("sfm_plane_sweep_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("sfm_plane_sweep", ctypes.c_int,
      [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
-      ctypes.c_float, ctypes.c_int, _c_dp, _c_dp]),
+      ctypes.c_float, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),
     ("sfm_plane_sweep_warped", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
-      ctypes.c_float, ctypes.c_int, _c_dp, _c_dp]),
+      ctypes.c_float, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),
     ("sfm_inverse_warp", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp]),
     ("sfm_profile_enable", ctypes.c_int, [ctypes.c_int]),

@@ -40,6 +40,7 @@ class TwoViewHotPath:
         self.ws = ransac.workspace_for(B, self.iters, self.device)
         self.cost = torch.empty(B, 2 * self.C, self.L, self.h, self.w, dtype=cost_dtype, device=self.device)
         self.cost_dtype = cost_dtype
+        self.sweep_ws = sweep.workspace_for(B, self.C, self.h, self.w, self.device)
 
     def pose(self, flow, K):
         Kinv = torch.inverse(K.float())
@@ -55,7 +56,7 @@ class TwoViewHotPath:
         if self.rescale is not None:
             pose[:, :, -1:] = pose[:, :, -1:] * self.rescale
         return sweep.plane_sweep_cost(ref_fea, tgt_fea, pose, K4, Ki4, self.L, self.min_depth, self.cost_dtype,
-                                      out=self.cost)
+                                      out=self.cost, workspace=self.sweep_ws)
 
     def step(self, flow, K, ref_fea, tgt_fea):
         E, P, inl, win = self.pose(flow, K)

@@ -27,8 +27,14 @@ def check_sizes(t, name, expected):
     assert ok, "wrong size for {}, expected {}, got  {}".format(name, "x".join(expected), list(t.size()))
 
 
+def workspace_for(batch, channels, h, w, device):
+    """Reusable plane-sweep scratch (channel-quad copy of the target features)."""
+    n = _lib.load().sfm_plane_sweep_workspace_bytes(int(batch), int(channels), int(h), int(w))
+    return torch.empty(int(n), dtype=torch.uint8, device=device)
+
+
 def plane_sweep_cost(ref_fea, tgt_fea, pose, intrinsics4, intrinsics_inv4, nlabel, min_depth=1.0,
-                     dtype=torch.float32, out=None, warped_only=False):
+                     dtype=torch.float32, out=None, warped_only=False, workspace=None):
     """Cost volume [B, 2C, L, h, w] (or [B, C, L, h, w] with warped_only).
     ``pose`` [B,3,4] (already translation-rescaled), intrinsics at feature
     resolution.  ``dtype``: torch.float32 or torch.bfloat16."""
@@ -45,14 +51,18 @@ def plane_sweep_cost(ref_fea, tgt_fea, pose, intrinsics4, intrinsics_inv4, nlabe
         out = torch.empty(B, cout, int(nlabel), h, w, dtype=dtype, device=tgt.device)
     code = 0 if dtype == torch.float32 else 1
     L = _lib.load()
+    if workspace is None:
+        workspace = workspace_for(B, C, h, w, tgt.device)
     with torch.cuda.device(tgt.device):
         s = _lib.stream_ptr(tgt.device)
         if warped_only:
             rc = L.sfm_plane_sweep_warped(_lib.ptr(tgt), B, C, h, w, _lib.ptr(pose), _lib.ptr(K4), _lib.ptr(Ki4),
-                                          int(nlabel), float(min_depth), code, _lib.ptr(out), s)
+                                          int(nlabel), float(min_depth), code, _lib.ptr(out), _lib.ptr(workspace),
+                                          workspace.numel(), s)
         else:
             rc = L.sfm_plane_sweep(_lib.ptr(ref), _lib.ptr(tgt), B, C, h, w, _lib.ptr(pose), _lib.ptr(K4),
-                                   _lib.ptr(Ki4), int(nlabel), float(min_depth), code, _lib.ptr(out), s)
+                                   _lib.ptr(Ki4), int(nlabel), float(min_depth), code, _lib.ptr(out),
+                                   _lib.ptr(workspace), workspace.numel(), s)
         _lib.check(rc, "sfm_plane_sweep")
     return out
 

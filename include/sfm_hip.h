@@ -139,6 +139,10 @@ int sfm_essential_decompose_uv(const double* E, double* U, double* V);
 /* ------------------------------------------------------------------------
  * Plane sweep
  * ------------------------------------------------------------------------ */
+/* Scratch for the plane sweep: the target features re-laid out as channel
+ * quads [B][ceil(C/4)][h*w][4] float32. */
+size_t sfm_plane_sweep_workspace_bytes(int batch, int channels, int h, int w);
+
 /* Cost volume of models/PSNet.py:144-157 for one target view:
  *   cost[b, c,   i] = ref[b, c]                     (c < C)
  *   cost[b, C+c, i] = inverse_warp(tgt, d_i)[b, c]
@@ -150,12 +154,14 @@ int sfm_essential_decompose_uv(const double* E, double* U, double* V);
  *   cost     [dev] batch x 2C x nlabel x h x w */
 int sfm_plane_sweep(const float* ref, const float* tgt, int batch, int channels, int h, int w,
                     const float* pose, const float* K4, const float* K4inv,
-                    int nlabel, float min_depth, int out_dtype, void* cost, void* stream);
+                    int nlabel, float min_depth, int out_dtype, void* cost,
+                    void* workspace, size_t workspace_bytes, void* stream);
 
 /* Warped half only (cost[b, c, i] = inverse_warp(tgt, d_i)), batch x C x nlabel x h x w. */
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w,
                            const float* pose, const float* K4, const float* K4inv,
-                           int nlabel, float min_depth, int out_dtype, void* out, void* stream);
+                           int nlabel, float min_depth, int out_dtype, void* out,
+                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* models/inverse_warp.py:121-153 for an arbitrary depth map:
  *   feat [dev] B x C x h x w; depth [dev] B x h x w; pose [dev] B x 3 x 4;
@@ -172,7 +178,7 @@ int sfm_profile_enable(int on);
 int sfm_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of
  * kernel `name` ("ransac_solve", "ransac_chain", "ransac_score",
- * "ransac_select", "flow_to_points", "plane_sweep", ...). */
+ * "ransac_select", "flow_to_points", "plane_sweep", "sweep_tgt_quads", ...). */
 int sfm_profile_read(const char* name, double* total_ms, int* launches);
 
 #ifdef __cplusplus

@@ -1,0 +1,132 @@
+// Probe: HBM write bandwidth of the cost-volume store shapes on gfx950.
+// Writes a [B=8][64][128][94*311] fp32 volume (7.66 GB) with
+//   A) per-thread 2 px x 64 rows, float2 non-temporal stores (current sweep)
+//   B) same with plain stores
+//   C) per-thread 4 px, float4 stores, 16-B aligned windows (rows aligned per plane parity)
+//   D) flat contiguous float4 grid-stride memset-like stream (ceiling)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
+
+constexpr int B = 8, CH = 64, L = 128, HW = 94 * 311;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__global__ __launch_bounds__(256) void kA(float* out) {
+  const int pix_blocks = (HW + 511) / 512;
+  int bid = blockIdx.x;
+  const int b = bid % B; bid /= B;
+  const int pg = bid % (L / 16); const int pb = bid / (L / 16);
+  const int p0 = (pb * 256 + threadIdx.x) * 2;
+  if (pb >= pix_blocks || p0 >= HW) return;
+  float* O = out + (size_t)b * CH * L * HW + p0;
+  for (int l = pg * 16; l < pg * 16 + 16; ++l)
+    for (int c = 0; c < CH; ++c) {
+      f2 v = {(float)c, (float)l};
+      f2* d = (f2*)(O + ((size_t)c * L + l) * HW);
+      if (NT) __builtin_nontemporal_store(v, d); else *d = v;
+    }
+}
+
+// float4 windows: row base parity decides a 2-element shift
+__global__ __launch_bounds__(256) void kC(float* out) {
+  const int win = (HW + 3 + 1023) / 1024;   // 1024 px per block (256 thr x 4)
+  int bid = blockIdx.x;
+  const int b = bid % B; bid /= B;
+  const int pg = bid % (L / 16); const int pb = bid / (L / 16);
+  if (pb >= win) return;
+  for (int l = pg * 16; l < pg * 16 + 16; ++l) {
+    const size_t rb0 = ((size_t)(b * CH) * L + l) * HW;
+    const int shift = (int)(rb0 & 3);              // same for every channel row of plane l (L even)
+    const int p = (pb * 256 + threadIdx.x) * 4 - shift;
+    for (int c = 0; c < CH; ++c) {
+      float* row = out + ((size_t)(b * CH + c) * L + l) * HW;
+      f4 v = {(float)c, (float)l, 1.f, 2.f};
+      if (p >= 0 && p + 3 < HW) __builtin_nontemporal_store(v, (f4*)(row + p));
+      else for (int k = 0; k < 4; ++k) if (p + k >= 0 && p + k < HW) row[p + k] = v[k];
+    }
+  }
+}
+
+// float4 windows, c outer / l inner (consecutive planes of one channel are contiguous)
+template <bool NT, int LG>
+__global__ __launch_bounds__(256) void kG(float* out) {
+  const int win = (HW + 3 + 1023) / 1024;
+  int bid = blockIdx.x;
+  const int b = bid % B; bid /= B;
+  const int pg = bid % (L / LG); const int pb = bid / (L / LG);
+  if (pb >= win) return;
+  for (int c = 0; c < CH; ++c) {
+    for (int l = pg * LG; l < pg * LG + LG; ++l) {
+      const size_t rb = ((size_t)(b * CH + c) * L + l) * HW;
+      const int p = (pb * 256 + threadIdx.x) * 4 - (int)(rb & 3);
+      float* row = out + rb;
+      f4 v = {(float)c, (float)l, 1.f, 2.f};
+      if (p >= 0 && p + 3 < HW) { if (NT) __builtin_nontemporal_store(v, (f4*)(row + p)); else *(f4*)(row + p) = v; }
+      else for (int k = 0; k < 4; ++k) if (p + k >= 0 && p + k < HW) row[p + k] = v[k];
+    }
+  }
+}
+
+// C with plain stores
+__global__ __launch_bounds__(256) void kE(float* out) {
+  const int win = (HW + 3 + 1023) / 1024;
+  int bid = blockIdx.x;
+  const int b = bid % B; bid /= B;
+  const int pg = bid % (L / 16); const int pb = bid / (L / 16);
+  if (pb >= win) return;
+  for (int l = pg * 16; l < pg * 16 + 16; ++l) {
+    const size_t rb0 = ((size_t)(b * CH) * L + l) * HW;
+    const int shift = (int)(rb0 & 3);
+    const int p = (pb * 256 + threadIdx.x) * 4 - shift;
+    for (int c = 0; c < CH; ++c) {
+      float* row = out + ((size_t)(b * CH + c) * L + l) * HW;
+      f4 v = {(float)c, (float)l, 1.f, 2.f};
+      if (p >= 0 && p + 3 < HW) *(f4*)(row + p) = v;
+      else for (int k = 0; k < 4; ++k) if (p + k >= 0 && p + k < HW) row[p + k] = v[k];
+    }
+  }
+}
+
+__global__ void kD(f4* out, size_t n4) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    f4 v = {1.f, 2.f, 3.f, 4.f};
+    __builtin_nontemporal_store(v, out + i);
+  }
+}
+
+int main() {
+  const size_t n = (size_t)B * CH * L * HW;
+  float* out;
+  CK(hipMalloc(&out, n * 4));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  auto run = [&](const char* name, auto launch) {
+    launch(); CK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+      CK(hipEventRecord(a)); launch(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+      float ms; CK(hipEventElapsedTime(&ms, a, b)); best = ms < best ? ms : best;
+    }
+    printf("%-40s %8.3f ms  %8.1f GB/s\n", name, best, n * 4 / (best * 1e-3) / 1e9);
+    return 0;
+  };
+  const int gA = ((HW + 511) / 512) * (L / 16) * B;
+  const int gC = ((HW + 3 + 1023) / 1024) * (L / 16) * B;
+  run("A float2 nt, 2px x 64 rows", [&] { hipLaunchKernelGGL(kA<true>, dim3(gA), dim3(256), 0, 0, out); });
+  run("B float2 plain, 2px x 64 rows", [&] { hipLaunchKernelGGL(kA<false>, dim3(gA), dim3(256), 0, 0, out); });
+  run("C float4 nt aligned windows, 4px x 64 rows", [&] { hipLaunchKernelGGL(kC, dim3(gC), dim3(256), 0, 0, out); });
+  run("E float4 plain aligned windows", [&] { hipLaunchKernelGGL(kE, dim3(gC), dim3(256), 0, 0, out); });
+  run("G float4 plain, c outer l inner (16)", [&] { hipLaunchKernelGGL((kG<false, 16>), dim3(gC), dim3(256), 0, 0, out); });
+  run("H float4 nt, c outer l inner (16)", [&] { hipLaunchKernelGGL((kG<true, 16>), dim3(gC), dim3(256), 0, 0, out); });
+  run("I float4 plain, c outer l inner (8)", [&] { hipLaunchKernelGGL((kG<false, 8>), dim3(gC * 2), dim3(256), 0, 0, out); });
+  run("J float4 plain, c outer l inner (32)", [&] { hipLaunchKernelGGL((kG<false, 32>), dim3(gC / 2), dim3(256), 0, 0, out); });
+  run("D float4 nt flat stream", [&] { hipLaunchKernelGGL(kD, dim3(8192), dim3(256), 0, 0, (f4*)out, n / 4); });
+  run("D2 float4 nt flat stream (2048 blk)", [&] { hipLaunchKernelGGL(kD, dim3(2048), dim3(256), 0, 0, (f4*)out, n / 4); });
+  CK(hipFree(out));
+  return 0;
+}

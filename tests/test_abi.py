@@ -60,8 +60,11 @@ def test_argument_validation_is_loud():
     rc = lib.sfm_ransac5_packed(ctypes.c_void_p(8), 5, n, 1, 10, 10, 1, 1e-3, 1234, 1, None, 0,
                                 ctypes.c_void_p(8), ctypes.c_void_p(8), ctypes.c_void_p(8), None, None, None)
     assert rc == 1 and b"exceed" in lib.sfm_last_error()
-    rc = lib.sfm_plane_sweep(None, None, 1, 32, 10, 10, None, None, None, 8, 1.0, 0, None, None)
+    rc = lib.sfm_plane_sweep(None, None, 1, 32, 10, 10, None, None, None, 8, 1.0, 0, None, None, 0, None)
     assert rc == 1
+    rc = lib.sfm_plane_sweep(ctypes.c_void_p(8), ctypes.c_void_p(8), 1, 32, 10, 10, ctypes.c_void_p(8),
+                             ctypes.c_void_p(8), ctypes.c_void_p(8), 8, 1.0, 0, ctypes.c_void_p(8), None, 0, None)
+    assert rc == 3 and b"workspace" in lib.sfm_last_error()
     import essential_matrix
     with pytest.raises(RuntimeError, match="double"):
         essential_matrix.optimise(torch.zeros(4, 2), torch.zeros(4, 2), torch.eye(3), 1e-3, 0.0, 5)

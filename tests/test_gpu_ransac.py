@@ -134,3 +134,25 @@ def test_full_size_dense_pair(cuda):
     # the recovered pose is the true one up to the translation scale
     t = P[0, :, 3].cpu().numpy(); tg = pose[0, :, 3].numpy().astype(np.float64)
     assert abs(abs(np.dot(t, tg / np.linalg.norm(tg))) - 1.0) < 5e-2
+
+
+@pytest.mark.parametrize("thr,scale", [(1e-4, 1.0), (1e-2, 1.0), (3e-6, 1.0), (1e-3, 1e3), (1e-3, 1e-3)])
+def test_fast_path_guard_near_epipole(cuda, thr, scale):
+    """Forward motion puts the epipole in the image: half of the points are
+    sampled within a few pixels of it, where |Ex| -> 0 and the FMA fast path
+    must hand the decision to the exact path.  Coordinates are also scaled to
+    stress the M-dependent guard.  Scores must match the oracle exactly."""
+    rng = np.random.default_rng(int(thr * 1e6) + int(scale * 7))
+    n = 3000
+    X = np.c_[rng.normal(0, 0.002, n), rng.normal(0, 0.002, n), np.ones(n)]
+    X[: n // 2, :2] = rng.uniform(-0.8, 0.8, (n // 2, 2))
+    X = X * rng.uniform(2, 50, (n, 1))
+    t = np.array([0.001, -0.002, -1.0])
+    X2 = X + t
+    q = X[:, :2] / X[:, 2:]
+    qp = X2[:, :2] / X2[:, 2:] + rng.normal(0, 2e-4, (n, 2))
+    q, qp = q * scale, qp * scale
+    r = _ransac_gpu(q, qp, n, n, 2, thr, True, cuda)
+    ref = R.ransac5(q, qp, n, n, 2, thr)
+    assert r["winner"] == ref["winner"] and r["inliers"] == ref["inliers"]
+    assert np.array_equal(r["scores"], ref["hyp_score"])
