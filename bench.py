@@ -14,7 +14,9 @@ max-over-ranks timing reduction.
 Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel (RANSAC
 scoring, fp64 VALU); `roofline_sweep` the HBM-bound cost-volume kernel; both
 average launch durations come from HIP events recorded by libsfm_hip around
-every launch on the launching stream during the timed region.  The
+every launch on the launching stream during the timed region; `traffic` is
+the PMC-measured HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950
+correction) from the committed profiles/rNN_pmc.json of the same workload.  The
 `cpu_baseline` is the oracle (CPU restatement) on a bounded sample, rank 0 only.
 """
 import argparse
@@ -49,6 +51,21 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of the path's kernels from the newest committed PMC
+    summary (profiles/rNN_pmc.json, scripts/gpu_pmc.sh + scripts/pmc_summary.py;
+    counters need their own profiler pass, so they cannot be read live here).
+    Only reported for the default workload the summary was collected on."""
+    import glob
+    if (args.batch, args.nlabel, args.iters, args.cost_dtype) != (8, 128, 8, "fp32"):
+        return {}, None
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not fs:
+        return {}, None
+    k = json.load(open(fs[-1]))["kernels"]
+    return {n: v.get("hbm_bytes") for n, v in k.items()}, os.path.relpath(fs[-1], ROOT)
 
 
 def cpu_baseline(flow, K, ref_fea, tgt_fea, pose, args):
@@ -129,6 +146,7 @@ def main():
     sweep_bytes = B * (2 * C * args.nlabel * h * w * s + 2 * C * h * w * 4)
     sweep_gbs = sweep_bytes / (kt["plane_sweep"] * 1e-3) / 1e9
 
+    traffic, traffic_src = pmc_traffic(args)
     if rank == 0:
         pairs = world * B * args.steps
         out = {
@@ -150,11 +168,13 @@ def main():
                        "pairs_per_gpu": B, "global_batch": world * B, "parallelism": f"dp{world}"},
             "roofline": {"kernel": "ransac_score", "bound": "valu-fp64", "achieved": round(score_tflops, 3),
                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": round(score_tflops / PEAK_FP64_TFLOPS, 4),
-                         "traffic": None, "avg_launch_ms": round(score_ms, 4),
+                         "traffic": traffic.get("ransac_score"), "traffic_source": traffic_src,
+                         "avg_launch_ms": round(score_ms, 4),
                          "work": f"{evals} evals x {FLOP_PER_EVAL} FLOP per launch ({sum(cands)} candidate E)"},
             "roofline_sweep": {"kernel": "plane_sweep", "bound": "hbm", "achieved": round(sweep_gbs, 1),
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(sweep_gbs / PEAK_HBM_GBS, 4),
-                               "traffic": None, "avg_launch_ms": round(kt["plane_sweep"], 4),
+                               "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,
+                               "avg_launch_ms": round(kt["plane_sweep"], 4),
                                "bytes_per_launch": sweep_bytes},
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "inliers": [int(v) for v in inl.cpu()],

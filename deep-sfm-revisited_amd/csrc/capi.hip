@@ -10,6 +10,11 @@ static thread_local std::string g_error;
 
 void set_error(const std::string& msg) { g_error = msg; }
 
+Tuning& tuning() {
+  static Tuning t;
+  return t;
+}
+
 namespace {
 struct Slot {
   std::string name;
@@ -76,6 +81,19 @@ extern "C" {
 int sfm_abi_version(void) { return SFM_ABI_VERSION; }
 
 const char* sfm_last_error(void) { return sfm::g_error.c_str(); }
+
+int sfm_tune_set(const char* key, int value) {
+  if (!key) { sfm::set_error("sfm_tune_set: null key"); return SFM_ERR_ARG; }
+  const std::string k(key);
+  sfm::Tuning& t = sfm::tuning();
+  if (k == "solve_lanes" && value >= 1 && value <= 64) t.solve_lanes = value;
+  else if (k == "sweep_lane_pixels" && (value == 0 || value == 1)) t.sweep_lane_pixels = value;
+  else if (k == "sweep_items_per_block" && (value == 1 || value == 2 || value == 4 || value == 8))
+    t.sweep_items_per_block = value;
+  else if (k == "score_blocks_per_cu" && value >= 1 && value <= 64) t.score_blocks_per_cu = value;
+  else { sfm::set_error("sfm_tune_set: unknown key or value out of range: " + k); return SFM_ERR_ARG; }
+  return SFM_OK;
+}
 
 int sfm_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(sfm::g_mu);

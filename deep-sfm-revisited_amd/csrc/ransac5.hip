@@ -89,12 +89,17 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
 // ---------------------------------------------------------------------------
 // Phase 1: one lane per hypothesis
 // ---------------------------------------------------------------------------
+// The solve is latency-bound (scratch-resident polynomial state, data-dependent
+// Sturm iterations): only `lanes` lanes of each wave carry a hypothesis, so a
+// pair's 4096 hypotheses occupy 4096 / lanes waves and every CU has several
+// independent instruction streams to hide the scratch latency.
 __global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, int64_t n_stride,
-                                              PairParams pp, int H, uint64_t seed, int cheir,
+                                              PairParams pp, int H, uint64_t seed, int cheir, int lanes,
                                               int32_t* __restrict__ out_nroots, int32_t* __restrict__ out_ncand,
                                               double* __restrict__ hypE, double* __restrict__ hypP) {
   const int b = blockIdx.y;
-  const int h = blockIdx.x * 64 + threadIdx.x;
+  if ((int)threadIdx.x >= lanes) return;
+  const int h = blockIdx.x * lanes + threadIdx.x;
   if (h >= H) return;
   const int64_t n = pp.n[b];
   int64_t idx[5];
@@ -536,7 +541,9 @@ static int run_chunk(const double* pts, int64_t n_stride, const int64_t* n, int 
   }
   {
     ProfScope ps("ransac_solve", s);
-    hipLaunchKernelGGL(k_solve, dim3((H + 63) / 64, bc), dim3(64), 0, s, pts, n_stride, pp, H, seed, cheir,
+    const int lanes = tuning().solve_lanes;
+    hipLaunchKernelGGL(k_solve, dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, pts, n_stride, pp, H, seed, cheir,
+                       lanes,
                        w.nroots, w.ncand, w.hypE, w.hypP);
   }
   SFM_LAUNCHED();
@@ -553,7 +560,7 @@ static int run_chunk(const double* pts, int64_t n_stride, const int64_t* n, int 
   ScoreConsts kc{thr, (thr * thr) * (1.0 - 0x1p-22), (thr * thr) * (1.0 + 0x1p-22)};
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int grid = std::max(1, cus) * 8;
+  const int grid = std::max(1, cus) * tuning().score_blocks_per_cu;
   {
     ProfScope ps("ransac_score", s);
     if (fast)

@@ -12,6 +12,7 @@
 //   grid_sample bilinear, zeros padding, align_corners=True
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <algorithm>
 #include <string>
 #include "common.h"
 
@@ -86,20 +87,23 @@ __device__ __forceinline__ unsigned short to_bf16(float f) {
 }
 
 // ---------------------------------------------------------------------------
-// Cost volume, v2: the output is produced in address order.
+// Cost volume: the output is produced in address order.
 //
-// Work item = (pair b, 4-row channel group g, plane l, 1024-pixel window):
-// 256 threads x 4 consecutive pixels write four 4 KB row segments with
-// 16-byte stores.  Items are enumerated with the window fastest, then the
-// plane, then the group, then the pair, and each block takes kSwItems
-// consecutive items, so the chip streams through the [B, 2C, L, h, w] volume
-// roughly in address order (a volume written as thousands of scattered row
-// chunks tops out ~20% lower on MI355X: scripts/probe_store_bw.hip).
-//
-// Groups [0, C4) copy the reference features (rows c < C, identical for every
-// plane); groups [C4, 2 C4) are the warped target features: the 4 bilinear
-// taps of each pixel are read as float4 from the channel-quad layout
-// tq[B][C4][h*w][4] (one 16-byte load per tap per 4 channels).
+// The [B, 2C, L, h, w] volume is cut into work items of 1024 consecutive
+// pixels (256 threads x 4, one 16-byte store per thread per row):
+//   * reference rows c < C: one item = one row segment (pure copy)
+//   * warped rows: one item = the same segment of a channel QUAD (4 rows),
+//     so the sampling position, mask and bilinear taps of a pixel are computed
+//     once for 4 channels and each tap is one 16-byte load from the
+//     channel-quad layout tq[B][C4][h*w][4] of the target features.
+// Items are enumerated in the volume's memory order (window fastest, then
+// plane, then row / quad, then pair) and each block takes `ipb` consecutive
+// items, so the resident blocks sweep one contiguous window of the volume.
+// MI355X write bandwidth drops with the number of interleaved store streams
+// (scripts/probe_store_bw.hip: 1 stream 4.9 TB/s, 2 -> 4.5, 4 -> 4.0, many
+// scattered row chunks -> 3.7): the copy half therefore runs as a single
+// stream, the warped half as 4 (the price of sharing the taps; one row per
+// item would need ~45 VALU ops and 5 vector loads per output element).
 //
 // 16-byte alignment: a row starts at element ((b*rows + r)*L + l)*h*w.  With
 // h*w = 2 (mod 4) and L even, that is 2*(l & 1) (mod 4) for every row of the
@@ -109,7 +113,6 @@ __device__ __forceinline__ unsigned short to_bf16(float f) {
 constexpr int kSwThreads = 256;
 constexpr int kSwPix = 4;
 constexpr int kSwWin = kSwThreads * kSwPix;
-constexpr int kSwItems = 8;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -155,84 +158,158 @@ __device__ __forceinline__ void store_row(OutT* row, int p0, int hw, const float
   }
 }
 
-template <typename OutT, bool VEC>
-__global__ __launch_bounds__(kSwThreads) void k_sweep(const float* __restrict__ ref, const f32x4* __restrict__ tq,
-                                                      int B, int C, int C4, int h, int w,
-                                                      const float* __restrict__ pose, const float* __restrict__ K4,
-                                                      const float* __restrict__ K4inv, int L, float dmax,
-                                                      int with_ref, int shift_mode, OutT* __restrict__ out) {
-  const int hw = h * w;
-  const int npw = (hw + 3 + kSwWin - 1) / kSwWin;
-  const int groups = with_ref ? 2 * C4 : C4;
-  const int rows = with_ref ? 2 * C : C;
-  const int64_t per_group = (int64_t)L * npw;
-  const int64_t total = (int64_t)B * groups * per_group;
-  const int64_t first = (int64_t)blockIdx.x * kSwItems;
-  for (int it = 0; it < kSwItems; ++it) {
-    const int64_t item = first + it;
-    if (item >= total) return;
-    const int pw = (int)(item % npw);
-    int64_t r = item / npw;
-    const int l = (int)(r % L);
-    r /= L;
-    const int g = (int)(r % groups);
-    const int b = (int)(r / groups);
-    const int shift = shift_mode ? 2 * (l & 1) : 0;
-    const int p0 = pw * kSwWin - shift + threadIdx.x * kSwPix;
-    if (p0 >= hw) continue;
-    OutT* plane = out + ((size_t)b * rows * L + l) * hw;    // row r at plane + r * L * hw
-    const size_t rstride = (size_t)L * hw;
-    if (with_ref && g < C4) {
-      // reference half: rows 4g .. 4g+3
-      const float* R = ref + (size_t)b * C * hw;
+struct SweepGeom {
+  int B, C, C4, h, w, L;
+  int ref_rows;    // C (full volume) or 0 (warped half only)
+  int rows;        // output rows per plane: ref_rows + C
+  int groups;      // row groups per pair: ref_rows single rows + C4 quads
+  int npw;         // pixel windows per row
+  int shift_mode;  // 1: odd planes' windows shifted by 2 elements
+  float dmax;      // MIN_DEPTH * L
+};
+
+// one warped item: 4 channels of the window at plane l
+template <typename OutT, bool VEC, bool LANE_PIX>
+__device__ __forceinline__ void warp_quad(const f32x4* __restrict__ tq, const float* __restrict__ pose,
+                                          const float* __restrict__ K4, const float* __restrict__ K4inv,
+                                          const SweepGeom& g, int b, int q, int l, int p0, OutT* plane,
+                                          size_t rstride) {
+  const int hw = g.h * g.w;
+  Proj pr;
+  load_proj(pose, K4, K4inv, b, pr);
+  const float d = g.dmax / (float)(l + 1);
+  const f32x4* T = tq + ((size_t)b * g.C4 + q) * hw;
+  f32x4 acc[4];
+  // LANE_PIX: pixel j of this lane is p0 + j (one 16-byte store per row);
+  // otherwise the window's pixels are lane-consecutive (w0 + 64 j + lane, with
+  // w0 = the wave's 256-pixel span), so each gather instruction reads
+  // neighbouring source pixels, at the price of 4-byte stores.
+  const int wave_base = p0 - 4 * (int)(threadIdx.x & 63);
+  const int lane = (int)(threadIdx.x & 63);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int c = 4 * g + k;
-        if (c >= C) break;
-        float v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int p = min(max(p0 + j, 0), hw - 1);
-          v[j] = R[(size_t)c * hw + p];
-        }
-        store_row<OutT, VEC>(plane + (size_t)c * rstride, p0, hw, v);
-      }
-      continue;
+  for (int j = 0; j < 4; ++j) {
+    const int pj = LANE_PIX ? p0 + j : wave_base + 64 * j + lane;
+    const int p = min(max(pj, 0), hw - 1);
+    const float x = (float)(p % g.w), y = (float)(p / g.w);
+    float ray[3];
+    ray[0] = (pr.ki[0] * x + pr.ki[1] * y) + pr.ki[2];
+    ray[1] = (pr.ki[3] * x + pr.ki[4] * y) + pr.ki[5];
+    ray[2] = (pr.ki[6] * x + pr.ki[7] * y) + pr.ki[8];
+    float ix, iy;
+    acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (sample_pos(pr, ray, d, g.h, g.w, ix, iy)) {
+      Taps tp;
+      make_taps(ix, iy, g.h, g.w, tp);
+      const f32x4 t0 = T[tp.off[0]], t1 = T[tp.off[1]], t2 = T[tp.off[2]], t3 = T[tp.off[3]];
+      f32x4 a = tp.wt[0] * t0;
+      a = a + tp.wt[1] * t1;
+      a = a + tp.wt[2] * t2;
+      a = a + tp.wt[3] * t3;
+      acc[j] = a;
     }
-    const int q = with_ref ? g - C4 : g;
-    Proj pr;
-    load_proj(pose, K4, K4inv, b, pr);
-    const float d = dmax / (float)(l + 1);
-    const f32x4* T = tq + ((size_t)b * C4 + q) * hw;
-    f32x4 acc[4];
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = min(max(p0 + j, 0), hw - 1);
-      const float x = (float)(p % w), y = (float)(p / w);
-      float ray[3];
-      ray[0] = (pr.ki[0] * x + pr.ki[1] * y) + pr.ki[2];
-      ray[1] = (pr.ki[3] * x + pr.ki[4] * y) + pr.ki[5];
-      ray[2] = (pr.ki[6] * x + pr.ki[7] * y) + pr.ki[8];
-      float ix, iy;
-      acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      if (sample_pos(pr, ray, d, h, w, ix, iy)) {
-        Taps tp;
-        make_taps(ix, iy, h, w, tp);
-        const f32x4 t0 = T[tp.off[0]], t1 = T[tp.off[1]], t2 = T[tp.off[2]], t3 = T[tp.off[3]];
-        f32x4 a = tp.wt[0] * t0;
-        a = a + tp.wt[1] * t1;
-        a = a + tp.wt[2] * t2;
-        a = a + tp.wt[3] * t3;
-        acc[j] = a;
-      }
-    }
-    const int cbase = with_ref ? C : 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = 4 * q + k;
-      if (c >= C) break;
+  for (int k = 0; k < 4; ++k) {
+    const int c = 4 * q + k;
+    if (c >= g.C) break;
+    OutT* row = plane + (size_t)(g.ref_rows + c) * rstride;
+    if (LANE_PIX) {
       const float v[4] = {acc[0][k], acc[1][k], acc[2][k], acc[3][k]};
-      store_row<OutT, VEC>(plane + (size_t)(cbase + c) * rstride, p0, hw, v);
+      store_row<OutT, VEC>(row, p0, hw, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int pj = wave_base + 64 * j + lane;
+        if (pj >= 0 && pj < hw) store1(row + pj, acc[j][k]);
+      }
+    }
+  }
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// 4 reference pixels p0..p0+3 of a row starting at element `row_off` of `ref`.
+// Even-aligned interior windows use two 8-byte loads (4 scalar loads per
+// thread cap the copy at ~3.6 TB/s on MI355X: the address unit, not HBM, is
+// the limit); edges and odd alignments load element-wise with clamping.
+__device__ __forceinline__ void load_ref4(const float* __restrict__ ref, size_t row_off, int p0, int hw,
+                                          float (&v)[4]) {
+  if (p0 >= 0 && p0 + 3 < hw && ((row_off + (size_t)p0) & 1) == 0) {
+    const f32x2 a = *reinterpret_cast<const f32x2*>(ref + row_off + p0);
+    const f32x2 b = *reinterpret_cast<const f32x2*>(ref + row_off + p0 + 2);
+    v[0] = a[0]; v[1] = a[1]; v[2] = b[0]; v[3] = b[1];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = ref[row_off + min(max(p0 + j, 0), hw - 1)];
+  }
+}
+
+struct ItemPos {
+  int pw, l, grp, b;
+  __device__ __forceinline__ void decode(int item, const SweepGeom& g) {
+    pw = item % g.npw;
+    int r = item / g.npw;
+    l = r % g.L;
+    r /= g.L;
+    grp = r % g.groups;
+    b = r / g.groups;
+  }
+  __device__ __forceinline__ void next(const SweepGeom& g) {
+    if (++pw == g.npw) {
+      pw = 0;
+      if (++l == g.L) {
+        l = 0;
+        if (++grp == g.groups) { grp = 0; ++b; }
+      }
+    }
+  }
+};
+
+template <typename OutT, bool VEC, int IPB, bool LANE_PIX = true>
+__global__ __launch_bounds__(kSwThreads) void k_sweep(const float* __restrict__ ref, const f32x4* __restrict__ tq,
+                                                      const float* __restrict__ pose, const float* __restrict__ K4,
+                                                      const float* __restrict__ K4inv, SweepGeom g,
+                                                      OutT* __restrict__ out) {
+  const int hw = g.h * g.w;
+  const int total = g.B * g.groups * g.L * g.npw;   // < 2^31 (checked by the launcher)
+  const int first = blockIdx.x * IPB;
+  if (first >= total) return;
+  const size_t rstride = (size_t)g.L * hw;
+  ItemPos ip;
+  ip.decode(first, g);
+  ItemPos last;
+  last.decode(min(first + IPB, total) - 1, g);
+  if (first + IPB <= total && last.b == ip.b && last.grp < g.ref_rows) {
+    // copy block: every item is a reference row of pair b.  Issue all loads
+    // first (IPB x 16 bytes in flight per thread), then the stores.
+    float v[IPB][4];
+    int p0s[IPB];
+    OutT* dst[IPB];
+#pragma unroll
+    for (int it = 0; it < IPB; ++it) {
+      const int shift = g.shift_mode ? 2 * (ip.l & 1) : 0;
+      const int p0 = ip.pw * kSwWin - shift + (int)threadIdx.x * kSwPix;
+      p0s[it] = p0;
+      dst[it] = out + (((size_t)ip.b * g.rows + ip.grp) * g.L + ip.l) * hw;
+      load_ref4(ref, ((size_t)ip.b * g.C + ip.grp) * hw, p0, hw, v[it]);
+      ip.next(g);
+    }
+#pragma unroll
+    for (int it = 0; it < IPB; ++it)
+      if (p0s[it] < hw) store_row<OutT, VEC>(dst[it], p0s[it], hw, v[it]);
+    return;
+  }
+  for (int it = 0, item = first; it < IPB && item < total; ++it, ++item, ip.next(g)) {
+    const int shift = g.shift_mode ? 2 * (ip.l & 1) : 0;
+    const int p0 = ip.pw * kSwWin - shift + (int)threadIdx.x * kSwPix;
+    OutT* plane = out + ((size_t)ip.b * g.rows * g.L + ip.l) * hw;   // row c at plane + c * rstride
+    if (ip.grp < g.ref_rows) {
+      if (p0 >= hw) continue;
+      float v[4];
+      load_ref4(ref, ((size_t)ip.b * g.C + ip.grp) * hw, p0, hw, v);
+      store_row<OutT, VEC>(plane + (size_t)ip.grp * rstride, p0, hw, v);
+    } else {
+      warp_quad<OutT, VEC, LANE_PIX>(tq, pose, K4, K4inv, g, ip.b, ip.grp - g.ref_rows, ip.l, p0, plane, rstride);
     }
   }
 }
@@ -274,9 +351,28 @@ __global__ __launch_bounds__(kSweepThreads) void k_inverse_warp(const float* __r
   }
 }
 
+template <typename OutT, bool VEC, bool LP>
+static void launch_k_sweep_lp(int ipb, int64_t blocks, hipStream_t s, const float* ref, const f32x4* tq, const float* pose,
+                           const float* K4, const float* K4inv, const SweepGeom& g, void* out) {
+  const dim3 grid((unsigned)blocks), block(kSwThreads);
+  switch (ipb) {
+    case 1: hipLaunchKernelGGL((k_sweep<OutT, VEC, 1, LP>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
+    case 2: hipLaunchKernelGGL((k_sweep<OutT, VEC, 2, LP>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
+    case 4: hipLaunchKernelGGL((k_sweep<OutT, VEC, 4, LP>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
+    default: hipLaunchKernelGGL((k_sweep<OutT, VEC, 8, LP>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
+  }
+}
+
+template <typename OutT, bool VEC>
+static void launch_k_sweep(int ipb, int64_t blocks, hipStream_t s, const float* ref, const f32x4* tq, const float* pose,
+                           const float* K4, const float* K4inv, const SweepGeom& g, void* out) {
+  if (tuning().sweep_lane_pixels) launch_k_sweep_lp<OutT, VEC, true>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+  else launch_k_sweep_lp<OutT, VEC, false>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+}
+
 static size_t sweep_ws_bytes(int B, int C, int h, int w) {
   const int C4 = (C + 3) / 4;
-  return (size_t)B * C4 * (size_t)h * w * 16;
+  return (size_t)B * C4 * (size_t)h * w * sizeof(f32x4);
 }
 
 static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B, int C, int h, int w,
@@ -291,31 +387,38 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     set_error("plane sweep workspace too small: need " + std::to_string(need) + " bytes");
     return SFM_ERR_WORKSPACE;
   }
-  const int hw = h * w, C4 = (C + 3) / 4;
-  const int npw = (hw + 3 + kSwWin - 1) / kSwWin;
-  const int groups = with_ref ? 2 * C4 : C4;
-  const int64_t items = (int64_t)B * groups * L * npw;
-  const int64_t blocks = (items + kSwItems - 1) / kSwItems;
-  SFM_REQUIRE(blocks < ((int64_t)1 << 31), "sweep grid too large");
+  const int hw = h * w;
+  SweepGeom g;
+  g.B = B; g.C = C; g.C4 = (C + 3) / 4; g.h = h; g.w = w; g.L = L;
+  g.ref_rows = with_ref ? C : 0;
+  g.rows = g.ref_rows + C;
+  g.groups = g.ref_rows + g.C4;
+  g.npw = (hw + 3 + kSwWin - 1) / kSwWin;
   // 16-byte row alignment (see k_sweep): every row aligned if hw % 4 == 0; rows of
   // plane l shifted by 2*(l&1) if hw % 4 == 2 and L even; element stores otherwise
-  const bool vec = (hw % 4 == 0) || (hw % 4 == 2 && L % 2 == 0);
-  const int shift_mode = (hw % 4 == 2 && L % 2 == 0) ? 1 : 0;
-  const float dmax = min_depth * (float)L;   // disp2depth = ones * MIN_DEPTH * nlabel (fp32)
+  g.shift_mode = (hw % 4 == 2 && L % 2 == 0) ? 1 : 0;
+  const bool vec = (hw % 4 == 0) || g.shift_mode;
+  const int ipb = tuning().sweep_items_per_block >= 8 ? 8 : tuning().sweep_items_per_block >= 4 ? 4
+                  : tuning().sweep_items_per_block >= 2 ? 2 : 1;
+  g.dmax = min_depth * (float)L;   // disp2depth = ones * MIN_DEPTH * nlabel (fp32)
+  const int64_t items = (int64_t)B * g.groups * L * g.npw;
+  SFM_REQUIRE(items < ((int64_t)1 << 31), "sweep too large for one launch");
+  const int64_t blocks = (items + ipb - 1) / ipb;
   f32x4* tq = (f32x4*)ws;
   {
     ProfScope ps("sweep_tgt_quads", s);
-    const int64_t n = (int64_t)B * C4 * hw;
-    hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tgt, B, C, C4, hw, tq);
+    const int64_t n = (int64_t)B * g.C4 * hw;
+    hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tgt, B, C, g.C4, hw, tq);
   }
   SFM_LAUNCHED();
   ProfScope ps(with_ref ? "plane_sweep" : "plane_sweep_warped", s);
-#define SFM_SWEEP_LAUNCH(OT, V)                                                                              \
-  hipLaunchKernelGGL((k_sweep<OT, V>), dim3((unsigned)blocks), dim3(kSwThreads), 0, s, ref, tq, B, C, C4, h, w, \
-                     pose, K4, K4inv, L, dmax, with_ref ? 1 : 0, shift_mode, (OT*)out)
-  if (out_dtype == 0) { if (vec) SFM_SWEEP_LAUNCH(float, true); else SFM_SWEEP_LAUNCH(float, false); }
-  else { if (vec) SFM_SWEEP_LAUNCH(unsigned short, true); else SFM_SWEEP_LAUNCH(unsigned short, false); }
-#undef SFM_SWEEP_LAUNCH
+  if (out_dtype == 0) {
+    if (vec) launch_k_sweep<float, true>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+    else launch_k_sweep<float, false>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+  } else {
+    if (vec) launch_k_sweep<unsigned short, true>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+    else launch_k_sweep<unsigned short, false>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+  }
   SFM_LAUNCHED();
   return SFM_OK;
 }

@@ -46,6 +46,7 @@ _SIGS = [
       ctypes.c_float, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),
     ("sfm_inverse_warp", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp]),
+    ("sfm_tune_set", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("sfm_profile_enable", ctypes.c_int, [ctypes.c_int]),
     ("sfm_profile_reset", ctypes.c_int, []),
     ("sfm_profile_read", ctypes.c_int,
@@ -119,3 +120,8 @@ def profile_read(name):
     n = ctypes.c_int(0)
     check(load().sfm_profile_read(name.encode(), ctypes.byref(ms), ctypes.byref(n)), "sfm_profile_read")
     return ms.value, n.value
+
+
+def tune(key, value):
+    """Set a launch-shape knob of libsfm_hip (see sfm_tune_set in include/sfm_hip.h)."""
+    check(load().sfm_tune_set(key.encode(), int(value)), "sfm_tune_set")

@@ -170,6 +170,12 @@ int sfm_inverse_warp(const float* feat, int batch, int channels, int h, int w,
                      const float* depth, const float* pose, const float* K, const float* Kinv,
                      float* out, void* stream);
 
+/* Launch-shape tuning (process-wide): "solve_lanes" (1..64, default 32),
+ * "sweep_items_per_block" (1, 2, 4 or 8; default 4), "sweep_lane_pixels"
+ * (0/1, pixel-to-lane mapping of the warped rows), "score_blocks_per_cu"
+ * (1..64, default 32).  Results never depend on these. */
+int sfm_tune_set(const char* key, int value);
+
 /* ------------------------------------------------------------------------
  * Per-kernel timing (HIP events recorded around every launch on the
  * launching stream while enabled).

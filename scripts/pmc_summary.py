@@ -1,0 +1,68 @@
+"""Summarise the rocprofv3 --pmc passes of scripts/gpu_pmc.sh into one JSON
+per round (profiles/rNN_pmc.json): per-launch counters of the path's kernels.
+
+HBM traffic follows /opt/skills/guides/MI355X_MICROARCH.md (HBM/rocprofv3):
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the
+bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is taken as is
+(calibrated for 16-byte-per-lane stores; for the sweep it matches the
+algorithmic byte count of the volume to 0.2%).  Infinity-Cache hits are
+counted in FETCH_SIZE, so re-reads of L3-resident inputs show up there.
+
+usage: python scripts/pmc_summary.py gpurun_out/pmc profiles/r01_pmc.json
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNELS = {"k_score": "ransac_score", "k_sweep": "plane_sweep", "k_solve": "ransac_solve",
+           "k_chain": "ransac_chain", "k_tgt_quads": "sweep_tgt_quads", "k_flow_points": "flow_to_points"}
+
+
+def kernel_key(name):
+    base = name.split("(")[0]
+    for k, v in KERNELS.items():
+        if base.endswith(k) or ("::" + k + "<") in base:
+            return v
+    return None
+
+
+def main(src, dst):
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True)):
+        acc = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            k = kernel_key(r["Kernel_Name"])
+            if k:
+                acc[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        for (k, _, c), v in acc.items():
+            per[k][c].append(v)
+    out = {}
+    for k, cs in per.items():
+        m = {c: sum(v) / len(v) for c, v in cs.items()}   # mean over dispatches
+        d = {"launches_sampled": max(len(v) for v in cs.values())}
+        d.update({c: round(v, 1) for c, v in sorted(m.items())})
+        if "FETCH_SIZE" in m:
+            d["hbm_read_bytes"] = int(m["FETCH_SIZE"] * 1024 * 2)
+        if "WRITE_SIZE" in m:
+            d["hbm_write_bytes"] = int(m["WRITE_SIZE"] * 1024)
+        if "hbm_read_bytes" in d and "hbm_write_bytes" in d:
+            d["hbm_bytes"] = d["hbm_read_bytes"] + d["hbm_write_bytes"]
+        if "TCC_HIT_sum" in m:
+            d["l2_hit_rate"] = round(m["TCC_HIT_sum"] / max(m["TCC_HIT_sum"] + m["TCC_MISS_sum"], 1), 4)
+        if "SQ_INSTS_VALU" in m and "SQ_WAVES" in m:
+            d["valu_insts_per_wave"] = round(m["SQ_INSTS_VALU"] / m["SQ_WAVES"], 1)
+        if "SQ_ACTIVE_INST_VALU" in m and "SQ_WAVE_CYCLES" in m:
+            d["valu_active_frac_of_wave_cycles"] = round(m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"], 4)
+        out[k] = d
+    json.dump({"source": "rocprofv3 --pmc --kernel-trace, separate passes (scripts/gpu_pmc.sh) over "
+                         "`python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline`",
+               "kernels": out}, open(dst, "w"), indent=1, sort_keys=True)
+    print(json.dumps({k: {x: v.get(x) for x in ("hbm_read_bytes", "hbm_write_bytes", "l2_hit_rate")}
+                      for k, v in out.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

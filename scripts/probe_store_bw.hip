@@ -92,6 +92,59 @@ __global__ __launch_bounds__(256) void kE(float* out) {
   }
 }
 
+// item order (b, g, l, pw) with pw fastest; each item writes RPI rows x 1024 px
+template <int RPI, int IPB, int CSTRIDE = 1>
+__global__ __launch_bounds__(256) void kItems(float* out) {
+  constexpr int NPW = (HW + 3 + 1023) / 1024;
+  constexpr int G = CH / RPI;
+  const int total = B * G * L * NPW;
+  for (int it = 0; it < IPB; ++it) {
+    const int item = blockIdx.x * IPB + it;
+    if (item >= total) return;
+    const int pw = item % NPW; int r = item / NPW;
+    const int l = r % L; r /= L;
+    const int g = r % G; const int b = r / G;
+    const int p = pw * 1024 - 2 * (l & 1) + threadIdx.x * 4;
+    for (int k = 0; k < RPI; ++k) {
+      const int c = CSTRIDE == 1 ? g * RPI + k : g + k * (CH / RPI);
+      float* row = out + ((size_t)(b * CH + c) * L + l) * HW;
+      f4 v = {(float)k, (float)l, 1.f, 2.f};
+      if (p >= 0 && p + 3 < HW) *(f4*)(row + p) = v;
+      else for (int j = 0; j < 4; ++j) if (p + j >= 0 && p + j < HW) row[p + j] = v[j];
+    }
+  }
+}
+
+// flat 1-row items copying a source row (re-read for every plane, L2-resident)
+// LD: 0 = no load (constant), 1 = 4 scalar loads, 2 = 2 x float2 loads
+template <int LD, int IPB>
+__global__ __launch_bounds__(256) void kCopy(const float* __restrict__ src, float* out) {
+  constexpr int NPW = (HW + 3 + 1023) / 1024;
+  const int total = B * CH * L * NPW;
+  for (int it = 0; it < IPB; ++it) {
+    const int item = blockIdx.x * IPB + it;
+    if (item >= total) return;
+    const int pw = item % NPW; int r = item / NPW;
+    const int l = r % L; r /= L;
+    const int c = r % CH; const int b = r / CH;
+    const int p = pw * 1024 - 2 * (l & 1) + threadIdx.x * 4;
+    const float* S = src + ((size_t)b * 32 + (c & 31)) * HW;
+    f4 v;
+    if (LD == 0) {
+      v = f4{(float)c, (float)l, 1.f, 2.f};
+    } else if (LD == 1) {
+      for (int j = 0; j < 4; ++j) v[j] = S[min(max(p + j, 0), HW - 1)];
+    } else {
+      const int q = min(max(p, 0), HW - 4);
+      const f2 a = *(const f2*)(S + (q & ~1)), bb = *(const f2*)(S + (q & ~1) + 2);
+      v = f4{a[0], a[1], bb[0], bb[1]};
+    }
+    float* row = out + ((size_t)(b * CH + c) * L + l) * HW;
+    if (p >= 0 && p + 3 < HW) *(f4*)(row + p) = v;
+    else for (int j = 0; j < 4; ++j) if (p + j >= 0 && p + j < HW) row[p + j] = v[j];
+  }
+}
+
 __global__ void kD(f4* out, size_t n4) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     f4 v = {1.f, 2.f, 3.f, 4.f};
@@ -117,16 +170,24 @@ int main() {
   };
   const int gA = ((HW + 511) / 512) * (L / 16) * B;
   const int gC = ((HW + 3 + 1023) / 1024) * (L / 16) * B;
-  run("A float2 nt, 2px x 64 rows", [&] { hipLaunchKernelGGL(kA<true>, dim3(gA), dim3(256), 0, 0, out); });
-  run("B float2 plain, 2px x 64 rows", [&] { hipLaunchKernelGGL(kA<false>, dim3(gA), dim3(256), 0, 0, out); });
-  run("C float4 nt aligned windows, 4px x 64 rows", [&] { hipLaunchKernelGGL(kC, dim3(gC), dim3(256), 0, 0, out); });
   run("E float4 plain aligned windows", [&] { hipLaunchKernelGGL(kE, dim3(gC), dim3(256), 0, 0, out); });
-  run("G float4 plain, c outer l inner (16)", [&] { hipLaunchKernelGGL((kG<false, 16>), dim3(gC), dim3(256), 0, 0, out); });
-  run("H float4 nt, c outer l inner (16)", [&] { hipLaunchKernelGGL((kG<true, 16>), dim3(gC), dim3(256), 0, 0, out); });
-  run("I float4 plain, c outer l inner (8)", [&] { hipLaunchKernelGGL((kG<false, 8>), dim3(gC * 2), dim3(256), 0, 0, out); });
-  run("J float4 plain, c outer l inner (32)", [&] { hipLaunchKernelGGL((kG<false, 32>), dim3(gC / 2), dim3(256), 0, 0, out); });
+  constexpr int NPW = (HW + 3 + 1023) / 1024;
+  run("P1 items 4 rows, ipb 4", [&] { hipLaunchKernelGGL((kItems<4, 4>), dim3((B * 16 * L * NPW + 3) / 4), dim3(256), 0, 0, out); });
+  run("P1s items 4 rows stride 16 ch, ipb 4", [&] { hipLaunchKernelGGL((kItems<4, 4, 16>), dim3((B * 16 * L * NPW + 3) / 4), dim3(256), 0, 0, out); });
+  run("P3 items 1 row (flat), ipb 4", [&] { hipLaunchKernelGGL((kItems<1, 4>), dim3((B * 64 * L * NPW + 3) / 4), dim3(256), 0, 0, out); });
+  run("P4 items 2 rows, ipb 4", [&] { hipLaunchKernelGGL((kItems<2, 4>), dim3((B * 32 * L * NPW + 3) / 4), dim3(256), 0, 0, out); });
   run("D float4 nt flat stream", [&] { hipLaunchKernelGGL(kD, dim3(8192), dim3(256), 0, 0, (f4*)out, n / 4); });
-  run("D2 float4 nt flat stream (2048 blk)", [&] { hipLaunchKernelGGL(kD, dim3(2048), dim3(256), 0, 0, (f4*)out, n / 4); });
+  float* src;
+  CK(hipMalloc(&src, (size_t)B * 32 * HW * 4));
+  {
+    std::vector<float> h((size_t)B * 32 * HW);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = (float)((i * 2654435761u) % 1000) * 0.001f + 0.5f;
+    CK(hipMemcpy(src, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  }
+  run("C0 copy items, no load, ipb 4", [&] { hipLaunchKernelGGL((kCopy<0, 4>), dim3((B * 64 * L * NPW + 3) / 4), dim3(256), 0, 0, src, out); });
+  run("C1 copy items, 4 scalar loads, ipb 4", [&] { hipLaunchKernelGGL((kCopy<1, 4>), dim3((B * 64 * L * NPW + 3) / 4), dim3(256), 0, 0, src, out); });
+  run("C2 copy items, 2 float2 loads, ipb 4", [&] { hipLaunchKernelGGL((kCopy<2, 4>), dim3((B * 64 * L * NPW + 3) / 4), dim3(256), 0, 0, src, out); });
+  CK(hipFree(src));
   CK(hipFree(out));
   return 0;
 }
