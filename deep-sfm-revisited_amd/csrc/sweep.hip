@@ -166,6 +166,7 @@ struct SweepGeom {
   int npw;         // pixel windows per row
   int shift_mode;  // 1: odd planes' windows shifted by 2 elements
   float dmax;      // MIN_DEPTH * L
+  float dstep;     // > 0: PREDICT_BY_DEPTH planes d_i = (i + 1) * dstep
 };
 
 // one warped item: 4 channels of the window at plane l
@@ -177,7 +178,8 @@ __device__ __forceinline__ void warp_quad(const f32x4* __restrict__ tq, const fl
   const int hw = g.h * g.w;
   Proj pr;
   load_proj(pose, K4, K4inv, b, pr);
-  const float d = g.dmax / (float)(l + 1);
+  // PSNet.py:150-153: depth planes (i+1)*MIN_DEPTH, or disp2depth / (i+1)
+  const float d = g.dstep > 0.0f ? (float)(l + 1) * g.dstep : g.dmax / (float)(l + 1);
   const f32x4* T = tq + ((size_t)b * g.C4 + q) * hw;
   f32x4 acc[4];
   // LANE_PIX: pixel j of this lane is p0 + j (one 16-byte store per row);
@@ -377,10 +379,12 @@ static size_t sweep_ws_bytes(int B, int C, int h, int w) {
 
 static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B, int C, int h, int w,
                         const float* pose, const float* K4, const float* K4inv, int L, float min_depth,
-                        int out_dtype, void* out, void* ws, size_t ws_bytes, hipStream_t s) {
+                        int depth_mode, int out_dtype, void* out, void* ws, size_t ws_bytes, hipStream_t s) {
   SFM_REQUIRE(tgt && pose && K4 && K4inv && out && (!with_ref || ref), "null pointer argument");
   SFM_REQUIRE(B >= 1 && C >= 1 && h >= 2 && w >= 2 && L >= 1, "invalid sweep shape");
   SFM_REQUIRE(out_dtype == 0 || out_dtype == 1, "out_dtype must be 0 (float32) or 1 (bfloat16)");
+  SFM_REQUIRE(depth_mode == 0 || depth_mode == 1, "depth_mode must be 0 (inverse depth) or 1 (depth)");
+  SFM_REQUIRE(min_depth > 0.0f, "min_depth must be positive");
   SFM_REQUIRE((int64_t)h * w < ((int64_t)1 << 30), "feature map too large");
   const size_t need = sweep_ws_bytes(B, C, h, w);
   if (!ws || ws_bytes < need) {
@@ -401,6 +405,7 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   const int ipb = tuning().sweep_items_per_block >= 8 ? 8 : tuning().sweep_items_per_block >= 4 ? 4
                   : tuning().sweep_items_per_block >= 2 ? 2 : 1;
   g.dmax = min_depth * (float)L;   // disp2depth = ones * MIN_DEPTH * nlabel (fp32)
+  g.dstep = depth_mode ? min_depth : 0.0f;
   const int64_t items = (int64_t)B * g.groups * L * g.npw;
   SFM_REQUIRE(items < ((int64_t)1 << 31), "sweep too large for one launch");
   const int64_t blocks = (items + ipb - 1) / ipb;
@@ -434,17 +439,26 @@ size_t sfm_plane_sweep_workspace_bytes(int batch, int channels, int h, int w) {
   return sweep_ws_bytes(batch, channels, h, w);
 }
 
+int sfm_plane_sweep_ex(const float* ref, const float* tgt, int batch, int channels, int h, int w,
+                       const float* pose, const float* K4, const float* K4inv, int nlabel, float min_depth,
+                       int depth_mode, int out_dtype, void* cost, void* workspace, size_t workspace_bytes,
+                       void* stream) {
+  return launch_sweep(ref != nullptr, ref, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth,
+                      depth_mode, out_dtype, cost, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
 int sfm_plane_sweep(const float* ref, const float* tgt, int batch, int channels, int h, int w, const float* pose,
                     const float* K4, const float* K4inv, int nlabel, float min_depth, int out_dtype, void* cost,
                     void* workspace, size_t workspace_bytes, void* stream) {
-  return launch_sweep(true, ref, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, out_dtype, cost,
+  SFM_REQUIRE(ref, "null pointer argument");
+  return launch_sweep(true, ref, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, 0, out_dtype, cost,
                       workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w, const float* pose,
                            const float* K4, const float* K4inv, int nlabel, float min_depth, int out_dtype,
                            void* out, void* workspace, size_t workspace_bytes, void* stream) {
-  return launch_sweep(false, nullptr, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, out_dtype,
+  return launch_sweep(false, nullptr, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, 0, out_dtype,
                       out, workspace, workspace_bytes, (hipStream_t)stream);
 }
 

@@ -41,6 +41,9 @@ _SIGS = [
     ("sfm_plane_sweep", ctypes.c_int,
      [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
       ctypes.c_float, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),
+    ("sfm_plane_sweep_ex", ctypes.c_int,
+     [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
+      ctypes.c_float, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),
     ("sfm_plane_sweep_warped", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
       ctypes.c_float, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),

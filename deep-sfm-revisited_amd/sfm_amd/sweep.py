@@ -34,35 +34,37 @@ def workspace_for(batch, channels, h, w, device):
 
 
 def plane_sweep_cost(ref_fea, tgt_fea, pose, intrinsics4, intrinsics_inv4, nlabel, min_depth=1.0,
-                     dtype=torch.float32, out=None, warped_only=False, workspace=None):
+                     dtype=torch.float32, out=None, warped_only=False, workspace=None, predict_by_depth=False):
     """Cost volume [B, 2C, L, h, w] (or [B, C, L, h, w] with warped_only).
     ``pose`` [B,3,4] (already translation-rescaled), intrinsics at feature
-    resolution.  ``dtype``: torch.float32 or torch.bfloat16."""
+    resolution.  ``dtype``: torch.float32 or torch.bfloat16.  Planes are
+    d_i = MIN_DEPTH*L/(i+1), or (i+1)*MIN_DEPTH with ``predict_by_depth``
+    (cfg.PREDICT_BY_DEPTH, PSNet.py:150-153)."""
     tgt = _dev_f32(tgt_fea, "tgt_fea")
     B, C, h, w = tgt.shape
     ref = None if warped_only else _dev_f32(ref_fea, "ref_fea")
+    if ref is not None and tuple(ref.shape) != (B, C, h, w):
+        raise RuntimeError(f"ref_fea shape {tuple(ref.shape)} != tgt_fea shape {(B, C, h, w)}")
     pose = _dev_f32(pose.reshape(B, 3, 4), "pose")
     K4 = _dev_f32(intrinsics4.reshape(B, 3, 3), "intrinsics")
     Ki4 = _dev_f32(intrinsics_inv4.reshape(B, 3, 3), "intrinsics_inv")
     if dtype not in (torch.float32, torch.bfloat16):
         raise RuntimeError("cost dtype must be float32 or bfloat16")
     cout = C if warped_only else 2 * C
+    shape = (B, cout, int(nlabel), h, w)
     if out is None:
-        out = torch.empty(B, cout, int(nlabel), h, w, dtype=dtype, device=tgt.device)
+        out = torch.empty(shape, dtype=dtype, device=tgt.device)
+    elif tuple(out.shape) != shape or out.dtype != dtype or not out.is_contiguous() or out.device != tgt.device:
+        raise RuntimeError(f"out must be a contiguous {dtype} tensor of shape {shape} on {tgt.device}")
     code = 0 if dtype == torch.float32 else 1
     L = _lib.load()
     if workspace is None:
         workspace = workspace_for(B, C, h, w, tgt.device)
     with torch.cuda.device(tgt.device):
-        s = _lib.stream_ptr(tgt.device)
-        if warped_only:
-            rc = L.sfm_plane_sweep_warped(_lib.ptr(tgt), B, C, h, w, _lib.ptr(pose), _lib.ptr(K4), _lib.ptr(Ki4),
-                                          int(nlabel), float(min_depth), code, _lib.ptr(out), _lib.ptr(workspace),
-                                          workspace.numel(), s)
-        else:
-            rc = L.sfm_plane_sweep(_lib.ptr(ref), _lib.ptr(tgt), B, C, h, w, _lib.ptr(pose), _lib.ptr(K4),
-                                   _lib.ptr(Ki4), int(nlabel), float(min_depth), code, _lib.ptr(out),
-                                   _lib.ptr(workspace), workspace.numel(), s)
+        rc = L.sfm_plane_sweep_ex(None if ref is None else _lib.ptr(ref), _lib.ptr(tgt), B, C, h, w, _lib.ptr(pose),
+                                  _lib.ptr(K4), _lib.ptr(Ki4), int(nlabel), float(min_depth),
+                                  1 if predict_by_depth else 0, code, _lib.ptr(out), _lib.ptr(workspace),
+                                  workspace.numel(), _lib.stream_ptr(tgt.device))
         _lib.check(rc, "sfm_plane_sweep")
     return out
 
@@ -101,8 +103,10 @@ def quarter_intrinsics(intrinsics, intrinsics_inv):
 class PlaneSweep(torch.nn.Module):
     """Sweep section of PSNet.forward (models/PSNet.py:128-158) on given features."""
 
-    def __init__(self, nlabel, mindepth=1.0, rescale_depth=False, norm_target=0.8, dtype=torch.float32):
+    def __init__(self, nlabel, mindepth=1.0, rescale_depth=False, norm_target=0.8, dtype=torch.float32,
+                 predict_by_depth=False):
         super().__init__()
+        self.predict_by_depth = predict_by_depth
         self.nlabel = int(nlabel)
         self.mindepth = float(mindepth)
         self.rescale_depth = rescale_depth
@@ -115,5 +119,6 @@ class PlaneSweep(torch.nn.Module):
         K4, Ki4 = quarter_intrinsics(intrinsics, intrinsics_inv)
         if self.rescale_depth:
             pose[:, 0, :, -1:] = pose[:, 0, :, -1:] * self.norm_target
-        return [plane_sweep_cost(ref_fea, t, pose[:, j], K4, Ki4, self.nlabel, self.mindepth, self.dtype)
+        return [plane_sweep_cost(ref_fea, t, pose[:, j], K4, Ki4, self.nlabel, self.mindepth, self.dtype,
+                                 predict_by_depth=self.predict_by_depth)
                 for j, t in enumerate(tgt_feas)]

@@ -157,6 +157,15 @@ int sfm_plane_sweep(const float* ref, const float* tgt, int batch, int channels,
                     int nlabel, float min_depth, int out_dtype, void* cost,
                     void* workspace, size_t workspace_bytes, void* stream);
 
+/* General form.  ref == NULL: warped half only, out batch x C x nlabel x h x w.
+ *   depth_mode 0: d_i = (min_depth * nlabel) / (i + 1)   (disp2depth, default)
+ *   depth_mode 1: d_i = (i + 1) * min_depth               (cfg.PREDICT_BY_DEPTH,
+ *                                                          PSNet.py:150-151) */
+int sfm_plane_sweep_ex(const float* ref, const float* tgt, int batch, int channels, int h, int w,
+                       const float* pose, const float* K4, const float* K4inv,
+                       int nlabel, float min_depth, int depth_mode, int out_dtype, void* cost,
+                       void* workspace, size_t workspace_bytes, void* stream);
+
 /* Warped half only (cost[b, c, i] = inverse_warp(tgt, d_i)), batch x C x nlabel x h x w. */
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w,
                            const float* pose, const float* K4, const float* K4inv,

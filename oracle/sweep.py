@@ -56,11 +56,12 @@ def quarter_intrinsics(K, Kinv):
 
 
 def plane_sweep_cost(ref_fea, tgt_fea, pose, K, Kinv, nlabel, min_depth=1.0, rescale=None,
-                     planes=None):
+                     planes=None, predict_by_depth=False):
     """Cost volume [B, 2C, L, h, w] (fp32).  ``pose`` [B,3,4]; K, Kinv are the
     full-resolution intrinsics (quartered here as PSNet does).  ``rescale``:
     NORM_TARGET factor applied to the translation (RESCALE_DEPTH) or None.
-    ``planes``: optional subset of plane indices (for bounded CPU baselines)."""
+    ``planes``: optional subset of plane indices (for bounded CPU baselines).
+    ``predict_by_depth``: cfg.PREDICT_BY_DEPTH planes (PSNet.py:150-151)."""
     K4, Ki4 = quarter_intrinsics(K, Kinv)
     pose = pose.clone()
     if rescale is not None:
@@ -71,7 +72,10 @@ def plane_sweep_cost(ref_fea, tgt_fea, pose, K, Kinv, nlabel, min_depth=1.0, res
     disp2depth = ones * min_depth * nlabel
     cost = torch.zeros(b, 2 * c, len(planes), h, w)
     for s, i in enumerate(planes):
-        depth = torch.div(disp2depth, i + 1 + 1e-16)
+        if predict_by_depth:
+            depth = ones * (i + 1) * min_depth                 # PSNet.py:151
+        else:
+            depth = torch.div(disp2depth, i + 1 + 1e-16)       # PSNet.py:153
         cost[:, :c, s] = ref_fea
         cost[:, c:, s] = inverse_warp(tgt_fea, depth, pose, K4, Ki4)
     return cost

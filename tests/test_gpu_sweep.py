@@ -103,3 +103,34 @@ def test_odd_pixel_count_and_warped_only(cuda):
     assert ok, err
     warped = plane_sweep_cost(None, tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 0.5, warped_only=True)
     assert torch.equal(warped, full[:, C:])
+
+
+@pytest.mark.parametrize("B,C,L,h,w,by_depth", [
+    (2, 8, 6, 12, 20, True),     # h*w % 4 == 0: every row 16-byte aligned
+    (2, 6, 5, 10, 31, False),    # h*w % 4 == 2 with odd L: element stores
+    (1, 3, 4, 10, 31, True),     # h*w % 4 == 2, even L: shifted windows, partial channel quad
+    (1, 36, 3, 40, 52, False),   # several quads, rows longer than one 1024-pixel window
+])
+def test_sweep_shapes_and_depth_modes(cuda, B, C, L, h, w, by_depth):
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
+    from sfm_amd import synth
+    ref, tgt = synth.features(B, C, h, w, seed=C + L)
+    K = synth.intrinsics(B, 4.0 * w, 4.0 * w, 2.0 * w, 2.0 * h)
+    Ki = torch.inverse(K)
+    pose = synth.relative_pose(B, torch.Generator().manual_seed(L))
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    got = plane_sweep_cost(ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 0.7,
+                           predict_by_depth=by_depth)
+    want = S.plane_sweep_cost(ref, tgt, pose, K, Ki, L, 0.7, predict_by_depth=by_depth)
+    assert torch.equal(got[:, :C].cpu(), want[:, :C])
+    ok, err = _close(got[:, C:], want[:, C:])
+    assert ok, err
+    assert float(want[:, C:].abs().sum()) > 0.0      # the poses project into the image
+
+
+def test_sweep_rejects_bad_out(cuda):
+    from sfm_amd.sweep import plane_sweep_cost
+    t = torch.zeros(1, 4, 8, 8, device=cuda)
+    P = torch.zeros(1, 3, 4, device=cuda); K = torch.eye(3, device=cuda).unsqueeze(0)
+    with pytest.raises(RuntimeError, match="out must be"):
+        plane_sweep_cost(t, t, P, K, K, 4, 1.0, out=torch.empty(1, 8, 3, 8, 8, device=cuda))
