@@ -5,86 +5,12 @@
 // with one launch that writes the whole [B, 2C, L, h, w] volume (plus a tiny
 // channel-quad relayout of the target features).  HBM-write-bound.
 //
-// Arithmetic follows the reference's float32 expression order:
-//   cam = (Kinv . (x, y, 1)) * d              pixel2cam (27-41)
-//   p   = (K.pose)[:, :3] . cam + (K.pose)[:, 3]   cam2pixel (44-75)
-//   Z clamped at 1e-3, xn = 2 (X/Z)/(w-1) - 1, |xn| > 1 -> 2 (zero sample)
-//   grid_sample bilinear, zeros padding, align_corners=True
-#include <hip/hip_runtime.h>
-#include <hip/hip_bf16.h>
+// Arithmetic: warp.h (the reference's float32 expression order).
 #include <algorithm>
 #include <string>
-#include "common.h"
+#include "warp.h"
 
 namespace sfm {
-
-constexpr int kSweepThreads = 256;
-
-struct Proj {   // (K . pose) rows and Kinv
-  float m[12];
-  float ki[9];
-};
-
-__device__ __forceinline__ void load_proj(const float* __restrict__ pose, const float* __restrict__ K,
-                                          const float* __restrict__ Kinv, int b, Proj& pr) {
-  const float* Pb = pose + b * 12;
-  const float* Kb = K + b * 9;
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      pr.m[4 * r + c] = (Kb[3 * r + 0] * Pb[c] + Kb[3 * r + 1] * Pb[4 + c]) + Kb[3 * r + 2] * Pb[8 + c];
-#pragma unroll
-  for (int e = 0; e < 9; ++e) pr.ki[e] = Kinv[b * 9 + e];
-}
-
-// Sampling position for a pixel ray `ray` (K^-1 (x,y,1)) at depth d.
-// Returns false when the sample is outside the image (the reference pushes the
-// normalised coordinate to 2 and grid_sample returns 0 for every channel).
-__device__ __forceinline__ bool sample_pos(const Proj& pr, const float ray[3], float d, int h, int w,
-                                           float& ix, float& iy) {
-  const float c0 = ray[0] * d, c1 = ray[1] * d, c2 = ray[2] * d;
-  const float X = ((pr.m[0] * c0 + pr.m[1] * c1) + pr.m[2] * c2) + pr.m[3];
-  const float Y = ((pr.m[4] * c0 + pr.m[5] * c1) + pr.m[6] * c2) + pr.m[7];
-  float Z = ((pr.m[8] * c0 + pr.m[9] * c1) + pr.m[10] * c2) + pr.m[11];
-  Z = Z < 1e-3f ? 1e-3f : Z;
-  const float xn = 2.0f * (X / Z) / (float)(w - 1) - 1.0f;
-  const float yn = 2.0f * (Y / Z) / (float)(h - 1) - 1.0f;
-  if (!(xn <= 1.0f && xn >= -1.0f && yn <= 1.0f && yn >= -1.0f)) return false;
-  ix = ((xn + 1.0f) / 2.0f) * (float)(w - 1);
-  iy = ((yn + 1.0f) / 2.0f) * (float)(h - 1);
-  return true;
-}
-
-struct Taps {
-  int off[4];
-  float wt[4];
-};
-
-__device__ __forceinline__ void make_taps(float ix, float iy, int h, int w, Taps& t) {
-  const float fx = floorf(ix), fy = floorf(iy);
-  const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
-  const float wx1 = ix - fx, wx0 = (fx + 1.0f) - ix;
-  const float wy1 = iy - fy, wy0 = (fy + 1.0f) - iy;
-  const bool vx0 = x0 >= 0 && x0 < w, vx1 = x1 >= 0 && x1 < w;
-  const bool vy0 = y0 >= 0 && y0 < h, vy1 = y1 >= 0 && y1 < h;
-  // nw, ne, sw, se (grid_sampler_2d order); invalid taps weight 0, clamped address
-  t.wt[0] = (vx0 && vy0) ? wx0 * wy0 : 0.0f;
-  t.wt[1] = (vx1 && vy0) ? wx1 * wy0 : 0.0f;
-  t.wt[2] = (vx0 && vy1) ? wx0 * wy1 : 0.0f;
-  t.wt[3] = (vx1 && vy1) ? wx1 * wy1 : 0.0f;
-  const int cx0 = min(max(x0, 0), w - 1), cx1 = min(max(x1, 0), w - 1);
-  const int cy0 = min(max(y0, 0), h - 1), cy1 = min(max(y1, 0), h - 1);
-  t.off[0] = cy0 * w + cx0;
-  t.off[1] = cy0 * w + cx1;
-  t.off[2] = cy1 * w + cx0;
-  t.off[3] = cy1 * w + cx1;
-}
-
-__device__ __forceinline__ unsigned short to_bf16(float f) {
-  __hip_bfloat16 b = __float2bfloat16(f);
-  return *reinterpret_cast<unsigned short*>(&b);
-}
 
 // ---------------------------------------------------------------------------
 // Cost volume: the output is produced in address order.
@@ -114,7 +40,6 @@ constexpr int kSwThreads = 256;
 constexpr int kSwPix = 4;
 constexpr int kSwWin = kSwThreads * kSwPix;
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // tgt [B][C][hw] -> tq [B][C4][hw] float4 (channels >= C are zero)
@@ -132,6 +57,12 @@ __global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4,
     v[k] = c < C ? tgt[((size_t)b * C + c) * hw + p] : 0.0f;
   }
   tq[i] = v;
+}
+
+void launch_channel_quads(const float* feat, int B, int C, int hw, f32x4* quads, hipStream_t s) {
+  const int C4 = (C + 3) / 4;
+  const int64_t n = (int64_t)B * C4 * hw;
+  hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, feat, B, C, C4, hw, quads);
 }
 
 __device__ __forceinline__ void store4(float* dst, const float (&v)[4]) {
@@ -412,8 +343,7 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   f32x4* tq = (f32x4*)ws;
   {
     ProfScope ps("sweep_tgt_quads", s);
-    const int64_t n = (int64_t)B * g.C4 * hw;
-    hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tgt, B, C, g.C4, hw, tq);
+    launch_channel_quads(tgt, B, C, hw, tq, s);
   }
   SFM_LAUNCHED();
   ProfScope ps(with_ref ? "plane_sweep" : "plane_sweep_warped", s);

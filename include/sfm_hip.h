@@ -172,6 +172,30 @@ int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int
                            int nlabel, float min_depth, int out_dtype, void* out,
                            void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Depth stage after the sweep
+ * ------------------------------------------------------------------------ */
+/* Scratch for sfm_plane_sweep_correlation: channel quads of ref and tgt. */
+size_t sfm_correlation_workspace_bytes(int batch, int channels, int h, int w);
+
+/* Correlation cost of REG2D.py:103-109 without the warped volume:
+ *   cost[b, i] = mean_c(ref[b, c] * inverse_warp(tgt, d_i)[b, c])
+ *   ref, tgt [dev] batch x C x h x w float32; pose/K4/K4inv as sfm_plane_sweep;
+ *   depth_mode as sfm_plane_sweep_ex; cost [dev] batch x nlabel x h x w float32. */
+int sfm_plane_sweep_correlation(const float* ref, const float* tgt, int batch, int channels, int h, int w,
+                                const float* pose, const float* K4, const float* K4inv, int nlabel,
+                                float min_depth, int depth_mode, float* cost,
+                                void* workspace, size_t workspace_bytes, void* stream);
+
+/* Soft-argmin depth head of PSNet.py:191-213 (submodule.py:57-93):
+ * F.interpolate(cost, [L, H, W], 'trilinear', align_corners=False) -> softmax
+ * over planes -> depth_mode 0: depth = min_depth*L / (sum p_i (i+1) + 1e-16)
+ *                depth_mode 1: depth = min_depth * sum p_i (i+1) depth_step
+ *                              (cfg.PREDICT_BY_DEPTH; depth_step = int(MIN_DEPTH))
+ *   cost [dev] batch x nlabel x h x w float32; depth [dev] batch x H x W float32. */
+int sfm_depth_head(const float* cost, int batch, int nlabel, int h, int w, int H, int W, int depth_mode,
+                   float min_depth, float depth_step, float* depth, void* stream);
+
 /* models/inverse_warp.py:121-153 for an arbitrary depth map:
  *   feat [dev] B x C x h x w; depth [dev] B x h x w; pose [dev] B x 3 x 4;
  *   K, Kinv [dev] B x 3 x 3; out [dev] B x C x h x w (float32). */

@@ -94,9 +94,41 @@ def flow2depth(R, T, flow, K):
     return out[:, -1, :, :]
 
 
-def depth_head(cost, nlabel, min_depth=1.0):
-    """Soft-argmin over planes of a cost [B, L, H, W] -> depth [B, 1, H, W]."""
-    prob = F.softmax(cost, dim=1)
-    disp = torch.arange(1, nlabel + 1, dtype=cost.dtype).view(1, nlabel, 1, 1)
-    d = torch.sum(prob * disp, 1)
-    return min_depth * nlabel / (d.unsqueeze(1) + 1e-16)
+def correlation_cost(ref_fea, tgt_fea, pose, K, Kinv, nlabel, min_depth=1.0, rescale=None,
+                     predict_by_depth=False):
+    """Parameter-free correlation cost of REG2D.py:103-109 (before its
+    leaky_relu): cost[:, i] = (ref * inverse_warp(tgt, d_i)).mean(1) with
+    quarter intrinsics; [B, L, h, w] fp32."""
+    K4, Ki4 = quarter_intrinsics(K, Kinv)
+    pose = pose.clone()
+    if rescale is not None:
+        pose[:, :, 3:] = pose[:, :, 3:] * rescale
+    b, c, h, w = ref_fea.shape
+    ones = torch.ones(b, h, w)
+    disp2depth = ones * min_depth * nlabel
+    cost = torch.zeros(b, nlabel, h, w)
+    for i in range(nlabel):
+        depth = ones * (i + 1) * min_depth if predict_by_depth else torch.div(disp2depth, i + 1 + 1e-16)
+        cost[:, i] = (ref_fea * inverse_warp(tgt_fea, depth, pose, K4, Ki4)).mean(dim=1)
+    return cost
+
+
+def depth_head(cost, nlabel, min_depth=1.0, out_hw=None, predict_by_depth=False):
+    """Soft-argmin head of PSNet.py:191-213 on a cost [B, L, h, w] (or
+    [B, 1, L, h, w]): trilinear upsample to [L, H, W] (align_corners=False),
+    softmax over planes, disparityregression / depthregression
+    (submodule.py:57-93) -> depth [B, 1, H, W]."""
+    if cost.dim() == 4:
+        cost = cost.unsqueeze(1)
+    B, _, L, h, w = cost.shape
+    H, W = (h, w) if out_hw is None else out_hw
+    up = F.interpolate(cost, [nlabel, H, W], mode="trilinear")
+    prob = F.softmax(torch.squeeze(up, 1), dim=1)
+    if predict_by_depth:
+        step = int(min_depth)
+        vals = torch.Tensor(np.reshape(np.array(range(1 * step, step * (nlabel + 1), step)), [1, nlabel, 1, 1]))
+        pred = torch.sum(prob * vals.expand(B, -1, H, W), 1)
+        return pred.unsqueeze(1) * min_depth
+    disp = torch.Tensor(np.reshape(np.array(range(1, nlabel + 1)), [1, nlabel, 1, 1]))
+    pred = torch.sum(prob * disp.expand(B, -1, H, W), 1)
+    return min_depth * nlabel / (pred.unsqueeze(1) + 1e-16)

@@ -1,0 +1,57 @@
+"""HIP depth stage (correlation cost + soft-argmin head) vs the oracle
+restatements of REG2D.py:103-109 and PSNet.py:191-213.  Floating-point bar
+(north_star): 1e-4 relative on the depth map."""
+import pytest
+import torch
+
+from oracle import sweep as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(B, C, h, w, seed):
+    from sfm_amd import synth
+    ref, tgt = synth.features(B, C, h, w, seed=seed)
+    K = synth.intrinsics(B, 4.0 * w, 4.0 * w, 2.0 * w, 2.0 * h)
+    pose = synth.relative_pose(B, torch.Generator().manual_seed(seed))
+    return ref, tgt, K, torch.inverse(K), pose
+
+
+@pytest.mark.parametrize("B,C,L,h,w,by_depth", [(2, 32, 16, 12, 20, False), (1, 6, 9, 10, 31, True),
+                                                 (1, 32, 128, 24, 78, False)])
+def test_correlation_cost(cuda, B, C, L, h, w, by_depth):
+    from sfm_amd.depth import correlation_cost
+    from sfm_amd.sweep import quarter_intrinsics
+    ref, tgt, K, Ki, pose = _scene(B, C, h, w, seed=L)
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    got = correlation_cost(ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 0.8,
+                           predict_by_depth=by_depth).cpu()
+    want = S.correlation_cost(ref, tgt, pose, K, Ki, L, 0.8, predict_by_depth=by_depth)
+    assert float(want.abs().max()) > 0.05
+    err = (got - want).abs() - (1e-4 * want.abs() + 2e-5)
+    assert float(err.max()) <= 0, float((got - want).abs().max())
+
+
+@pytest.mark.parametrize("B,L,h,w,H,W,by_depth", [(2, 16, 12, 20, 48, 80, False), (1, 128, 24, 78, 96, 312, False),
+                                                   (1, 10, 7, 9, 7, 9, True), (2, 12, 5, 6, 17, 23, False)])
+def test_depth_head(cuda, B, L, h, w, H, W, by_depth):
+    from sfm_amd.depth import depth_head
+    g = torch.Generator().manual_seed(L + h)
+    cost = torch.randn(B, L, h, w, generator=g) * 3.0
+    got = depth_head(cost.to(cuda), L, 1.0, (H, W), predict_by_depth=by_depth).cpu()
+    want = S.depth_head(cost, L, 1.0, (H, W), predict_by_depth=by_depth)
+    assert got.shape == want.shape == (B, 1, H, W)
+    rel = ((got - want).abs() / want.abs()).max()
+    assert float(rel) <= 1e-4, float(rel)
+
+
+def test_correlation_depth_module(cuda):
+    from sfm_amd.depth import CorrelationDepth
+    B, C, L, h, w = 2, 8, 24, 16, 40
+    ref, tgt, K, Ki, pose = _scene(B, C, h, w, seed=3)
+    m = CorrelationDepth(L, 1.0, rescale_depth=True, norm_target=0.6)
+    got = m(ref.to(cuda), tgt.to(cuda), pose.to(cuda), K.to(cuda), Ki.to(cuda), (4 * h, 4 * w)).cpu()
+    cost = S.correlation_cost(ref, tgt, pose, K, Ki, L, 1.0, rescale=0.6)
+    want = S.depth_head(cost, L, 1.0, (4 * h, 4 * w))
+    rel = ((got - want).abs() / want.abs()).max()
+    assert float(rel) <= 1e-4, float(rel)
