@@ -522,6 +522,81 @@ __global__ void k_flow_points(const float* __restrict__ flow, int H, int W, int 
   reinterpret_cast<double4*>(out)[(size_t)b * N + k] = make_double4(x1, y1, x2, y2);
 }
 
+// Sparse correspondences of SFMnet.pose_by_ransac (models/SFMnet.py:218-258):
+//   mode 0 (default): flow at the rounded keypoints of the reference image,
+//          pts1 = np.int32(np.round(kp))  ->  coord[:, y, x]           (250-253)
+//   mode 1 (cfg.SAMPLE_SP): grid_sample of the coordinate grids at the
+//          keypoints, align_corners=True, zeros padding             (242-247)
+//   mode 2 (cfg.SIFT_POSE): the matched keypoints themselves        (218-224)
+// followed by K^-1 (bmm, 3 rows) in float32 and the f64 widening of
+// compute_P_matrix_ransac.  Rows >= n[b] of the output are not written.
+struct KpCounts {
+  int n[SFM_MAX_BATCH];
+};
+
+__device__ __forceinline__ float kp_tap(float v, bool ok) { return ok ? v : 0.0f; }
+
+__global__ void k_keypoint_points(const float* __restrict__ flow, int H, int W, int h_side, int w_side,
+                                  const float* __restrict__ kp1, const float* __restrict__ kp2, int64_t kp_stride,
+                                  KpCounts cnt, int mode, const float* __restrict__ Kinv, double* __restrict__ out,
+                                  int64_t n_stride) {
+  const int b = blockIdx.y;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= cnt.n[b]) return;
+  const float* Ki = Kinv + b * 9;
+  const float* F = flow + (size_t)b * 2 * H * W;
+  const float kx = kp1[((size_t)b * kp_stride + k) * 2], ky = kp1[((size_t)b * kp_stride + k) * 2 + 1];
+  float c1[3], c2[3];
+  if (mode == 2) {
+    c1[0] = kx; c1[1] = ky; c1[2] = 1.0f;
+    c2[0] = kp2[((size_t)b * kp_stride + k) * 2]; c2[1] = kp2[((size_t)b * kp_stride + k) * 2 + 1]; c2[2] = 1.0f;
+  } else if (mode == 0) {
+    // round half to even (np.round); the caller validates the range (the
+    // reference's indexing raises), the clamp only keeps the access in bounds
+    const int x = min(max((int)rintf(kx), 0), w_side - 1);
+    const int y = min(max((int)rintf(ky), 0), h_side - 1);
+    const float fu = F[(size_t)y * W + x], fv = F[(size_t)H * W + (size_t)y * W + x];
+    c1[0] = (float)x; c1[1] = (float)y; c1[2] = 1.0f;
+    c2[0] = c1[0] + fu; c2[1] = c1[1] + fv; c2[2] = 1.0f;
+  } else {
+    // pts normalised in float32 as SFMnet.py:245, then grid_sample's
+    // align_corners=True unnormalisation and zero-padded bilinear taps
+    const float xn = 2.0f * kx / (float)max(w_side - 1, 1) - 1.0f;
+    const float yn = 2.0f * ky / (float)max(h_side - 1, 1) - 1.0f;
+    const float ix = ((xn + 1.0f) / 2.0f) * (float)(w_side - 1);
+    const float iy = ((yn + 1.0f) / 2.0f) * (float)(h_side - 1);
+    const float fx = floorf(ix), fy = floorf(iy);
+    const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+    const float wnw = ((fx + 1.0f) - ix) * ((fy + 1.0f) - iy);
+    const float wne = (ix - fx) * ((fy + 1.0f) - iy);
+    const float wsw = ((fx + 1.0f) - ix) * (iy - fy);
+    const float wse = (ix - fx) * (iy - fy);
+    const int xs[4] = {x0, x1, x0, x1}, ys[4] = {y0, y0, y1, y1};
+    const float wt[4] = {wnw, wne, wsw, wse};
+    float a1[3] = {0.0f, 0.0f, 0.0f}, a2[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bool ok = xs[t] >= 0 && xs[t] < w_side && ys[t] >= 0 && ys[t] < h_side;
+      const int xc = min(max(xs[t], 0), w_side - 1), yc = min(max(ys[t], 0), h_side - 1);
+      const float gx = (float)xc, gy = (float)yc;
+      const float fu = F[(size_t)yc * W + xc], fv = F[(size_t)H * W + (size_t)yc * W + xc];
+      a1[0] = a1[0] + kp_tap(gx, ok) * wt[t];
+      a1[1] = a1[1] + kp_tap(gy, ok) * wt[t];
+      a1[2] = a1[2] + kp_tap(1.0f, ok) * wt[t];
+      a2[0] = a2[0] + kp_tap(gx + fu, ok) * wt[t];
+      a2[1] = a2[1] + kp_tap(gy + fv, ok) * wt[t];
+      a2[2] = a2[2] + kp_tap(1.0f, ok) * wt[t];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { c1[j] = a1[j]; c2[j] = a2[j]; }
+  }
+  const float x1n = (Ki[0] * c1[0] + Ki[1] * c1[1]) + Ki[2] * c1[2];
+  const float y1n = (Ki[3] * c1[0] + Ki[4] * c1[1]) + Ki[5] * c1[2];
+  const float x2n = (Ki[0] * c2[0] + Ki[1] * c2[1]) + Ki[2] * c2[2];
+  const float y2n = (Ki[3] * c2[0] + Ki[4] * c2[1]) + Ki[5] * c2[2];
+  reinterpret_cast<double4*>(out)[(size_t)b * n_stride + k] = make_double4(x1n, y1n, x2n, y2n);
+}
+
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
@@ -716,6 +791,39 @@ int sfm_flow_to_points(const float* flow, int batch, int H, int W, int h_side, i
                        flow + (size_t)b0 * 2 * H * W, H, W, h_side, w_side, margin, Kinv + (size_t)b0 * 9,
                        pts_out + (size_t)b0 * N * 4);
   }
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+int sfm_keypoints_to_points(const float* flow, int batch, int H, int W, int h_side, int w_side,
+                            const float* kp1, const float* kp2, int64_t kp_stride, const int64_t* n, int mode,
+                            const float* Kinv, double* pts_out, int64_t n_stride, void* stream) {
+  SFM_REQUIRE(kp1 && n && Kinv && pts_out, "null pointer argument");
+  SFM_REQUIRE(mode >= 0 && mode <= 2, "mode must be 0 (rounded gather), 1 (SAMPLE_SP) or 2 (SIFT_POSE)");
+  SFM_REQUIRE(mode == 2 || flow, "null flow");
+  SFM_REQUIRE(mode != 2 || kp2, "SIFT_POSE needs the target keypoints");
+  SFM_REQUIRE(batch >= 1 && H >= 1 && W >= 1, "invalid flow shape");
+  SFM_REQUIRE(h_side >= 1 && h_side <= H && w_side >= 1 && w_side <= W, "h_side/w_side out of range");
+  int64_t nmax = 0;
+  for (int b = 0; b < batch; ++b) {
+    SFM_REQUIRE(n[b] >= 0 && n[b] <= kp_stride && n[b] <= n_stride && n[b] < (1 << 30),
+                "keypoint count out of range");
+    nmax = std::max(nmax, n[b]);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps("keypoints_to_points", s);
+  for (int b0 = 0; b0 < batch; b0 += SFM_MAX_BATCH) {
+    const int nb = std::min(SFM_MAX_BATCH, batch - b0);
+    KpCounts c;
+    int64_t m = 0;
+    for (int b = 0; b < nb; ++b) { c.n[b] = (int)n[b0 + b]; m = std::max(m, n[b0 + b]); }
+    if (m == 0) continue;
+    hipLaunchKernelGGL(k_keypoint_points, dim3((unsigned)((m + 255) / 256), nb), dim3(256), 0, s,
+                       mode == 2 ? nullptr : flow + (size_t)b0 * 2 * H * W, H, W, h_side, w_side,
+                       kp1 + (size_t)b0 * kp_stride * 2, mode == 2 ? kp2 + (size_t)b0 * kp_stride * 2 : nullptr,
+                       kp_stride, c, mode, Kinv + (size_t)b0 * 9, pts_out + (size_t)b0 * n_stride * 4, n_stride);
+  }
+  (void)nmax;
   SFM_LAUNCHED();
   return SFM_OK;
 }

@@ -47,6 +47,9 @@ _SIGS = [
     ("sfm_plane_sweep_warped", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
       ctypes.c_float, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),
+    ("sfm_keypoints_to_points", ctypes.c_int,
+     [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, ctypes.c_int64,
+      _c_dp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_int64, _c_dp]),
     ("sfm_correlation_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("sfm_plane_sweep_correlation", ctypes.c_int,
      [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,

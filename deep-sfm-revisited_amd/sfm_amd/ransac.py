@@ -150,3 +150,62 @@ def candidate_counts(workspace, batch, iters):
     _lib.check(_lib.load().sfm_ransac5_candidate_counts(_lib.ptr(workspace), workspace.numel(), int(batch),
                                                         int(iters), out), "sfm_ransac5_candidate_counts")
     return [int(v) for v in out]
+
+
+KEYPOINT_MODES = {"round": 0, "sample_sp": 1, "sift_pose": 2}
+
+
+def keypoints_to_points(flow, intrinsic_inv, kp1, kp2=None, mode="round", h_side=None, w_side=None, out=None):
+    """Sparse correspondences of SFMnet.pose_by_ransac (models/SFMnet.py:218-258)
+    for per-pair keypoint lists (any matcher; the reference uses cv2 SIFT/SURF).
+
+    kp1 / kp2: lists (one per pair) of [n_b, 2] pixel (x, y) arrays of the
+    reference / target image.  mode: "round" (default: flow at np.round(kp1)),
+    "sample_sp" (cfg.SAMPLE_SP bilinear), "sift_pose" (cfg.SIFT_POSE: kp1, kp2
+    directly).  Returns (pts [B, n_max, 4] float64, n list)."""
+    import numpy as np
+    m = KEYPOINT_MODES[mode]
+    if not intrinsic_inv.is_cuda:
+        raise RuntimeError("intrinsic_inv must be a CUDA tensor")
+    dev = intrinsic_inv.device
+    Ki = intrinsic_inv.contiguous().float()
+    B = Ki.shape[0]
+    if len(kp1) != B or (m == 2 and (kp2 is None or len(kp2) != B)):
+        raise RuntimeError("one keypoint array per pair is required")
+    if m != 2:
+        if not flow.is_cuda:
+            raise RuntimeError("flow must be a CUDA tensor")
+        flow = flow.contiguous().float()
+        _, _, H, W = flow.shape
+    else:
+        H = int(h_side or 1); W = int(w_side or 1)
+    h = H if h_side is None else int(h_side)
+    w = W if w_side is None else int(w_side)
+    n = [int(np.asarray(k).reshape(-1, 2).shape[0]) for k in kp1]
+    nmax = max(max(n), 1)
+    a1 = np.zeros((B, nmax, 2), np.float32)
+    a2 = np.zeros((B, nmax, 2), np.float32)
+    for b in range(B):
+        k = np.asarray(kp1[b], dtype=np.float64).reshape(-1, 2)
+        if m == 0:
+            # np.int32(np.round(pts)) then coord[:, y, x]: torch indexing wraps
+            # negative indices and raises past the end (SFMnet.py:250-253)
+            r = np.int32(np.round(k))
+            for j, size in ((0, w), (1, h)):
+                if np.any(r[:, j] >= size) or np.any(r[:, j] < -size):
+                    raise IndexError(f"keypoint index out of range for size {size}")
+                r[:, j] = np.where(r[:, j] < 0, r[:, j] + size, r[:, j])
+            k = r
+        a1[b, :n[b]] = k
+        if m == 2:
+            a2[b, :n[b]] = np.asarray(kp2[b], dtype=np.float32).reshape(-1, 2)
+    t1 = torch.from_numpy(a1).to(dev)
+    t2 = torch.from_numpy(a2).to(dev) if m == 2 else None
+    if out is None:
+        out = torch.zeros(B, nmax, 4, dtype=torch.float64, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.load().sfm_keypoints_to_points(
+            None if m == 2 else _lib.ptr(flow), B, H, W, h, w, _lib.ptr(t1), None if t2 is None else _lib.ptr(t2),
+            nmax, _lib.i64_array(n), m, _lib.ptr(Ki), _lib.ptr(out), out.shape[1], _lib.stream_ptr(dev)),
+            "sfm_keypoints_to_points")
+    return out, n

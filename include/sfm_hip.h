@@ -114,6 +114,22 @@ int sfm_ransac5_inlier_mask(const double* pts, int64_t n_stride, const int64_t* 
 int sfm_flow_to_points(const float* flow, int batch, int H, int W, int h_side, int w_side,
                        int margin, const float* Kinv, double* pts_out, void* stream);
 
+/* Sparse correspondences of SFMnet.pose_by_ransac (models/SFMnet.py:218-258),
+ * for keypoints from any matcher (the reference uses cv2 SIFT/SURF + FLANN):
+ *   mode 0: flow at np.round(kp1) (round half to even; caller validates the
+ *           range — the reference's indexing raises), cfg default;
+ *   mode 1: cfg.SAMPLE_SP — grid_sample (align_corners=True, zeros) of the
+ *           coordinate grids at kp1;
+ *   mode 2: cfg.SIFT_POSE — the matched keypoints kp1 / kp2 themselves;
+ * then K^-1 (float32, 3 rows) and f64 widening.
+ *   flow [dev] batch x 2 x H x W float32 (unused for mode 2), cropped to
+ *   h_side x w_side; kp1, kp2 [dev] batch x kp_stride x 2 float32 pixel (x, y);
+ *   n [host] batch int64 keypoints per pair; Kinv [dev] batch x 3 x 3 float32;
+ *   pts_out [dev] batch x n_stride x 4 float64 (rows >= n[b] untouched). */
+int sfm_keypoints_to_points(const float* flow, int batch, int H, int W, int h_side, int w_side,
+                            const float* kp1, const float* kp2, int64_t kp_stride, const int64_t* n, int mode,
+                            const float* Kinv, double* pts_out, int64_t n_stride, void* stream);
+
 /* Scored candidate E's per pair of the last sfm_ransac5_packed call made with
  * this workspace (the last <= SFM_MAX_BATCH chunk), copied to the host
  * (synchronous).  Work accounting: the score kernel evaluates

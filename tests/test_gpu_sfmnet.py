@@ -1,0 +1,143 @@
+"""SFMnet mirror (models/SFMnet.py) with injected flow / depth estimators and
+matcher: the pose branch through libsfm_hip vs the oracle pipeline (oracle
+correspondences -> oracle RANSAC per pair), bit-exact on E and P; the
+keypoint gather modes vs oracle/flow.py; the reference's return tuples."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import flow as OF
+from oracle import ransac5 as ORR
+
+pytestmark = pytest.mark.gpu
+
+HW = (96, 160)
+
+
+def _batch(B, seed):
+    from sfm_amd import synth
+    flow, K, pose, _ = synth.kitti_pair_batch(B, seed=seed, hw=HW)
+    K = synth.intrinsics(B, 180.0, 180.0, 80.0, 48.0)
+    return flow, K, pose
+
+
+class _Flow(torch.nn.Module):
+    def __init__(self, flow):
+        super().__init__()
+        self.flow = flow
+
+    def forward(self, x):
+        return self.flow.to(x.device), torch.ones_like(self.flow[:, :1]).to(x.device)
+
+
+class _Depth(torch.nn.Module):
+    def forward(self, ref, targets, P_mat, K, Kinv, pose_gt=None, depth_gt=None, E_mat=None):
+        self.seen = (P_mat.clone(), None if E_mat is None else E_mat.clone())
+        d = torch.ones(ref.shape[0], 1, ref.shape[2], ref.shape[3], device=ref.device)
+        return d, 2 * d
+
+
+def _model(flow, matcher=None, **over):
+    from models.SFMnet import SFMnet
+    from sfm_amd.config import defaults
+    c = defaults()
+    c.update(ransac_iter=2, **over)
+    return SFMnet(64, 1.0, flow_estimator=_Flow(flow), depth_estimator=_Depth(), matcher=matcher, cfg=c).eval()
+
+
+def _oracle_pose(q, qp, iters, thr):
+    r = ORR.ransac5(q, qp, iters=iters, thr=thr)
+    return r["E"].astype(np.float32), r["P"].astype(np.float32)
+
+
+def test_dense_pose_matches_oracle(cuda):
+    B = 3
+    flow, K, pose = _batch(B, seed=11)
+    m = _model(flow)
+    img = torch.zeros(B, 3, *HW, device=cuda)
+    flow_2D, P_mat, depth, times = m(img, img, K, pose_gt=pose.to(cuda))
+    assert P_mat.shape == (B, 1, 3, 4) and P_mat.dtype == torch.float32
+    assert depth.shape == (B, 1, *HW) and float(depth[0, 0, 0, 0]) == 2.0
+    Ki = torch.inverse(K.float())
+    q, qp = OF.dense_correspondences(flow.numpy(), Ki.numpy())
+    for b in range(B):
+        E, P = _oracle_pose(q[b], qp[b], 2, 1e-4)
+        assert np.array_equal(P_mat[b, 0].cpu().numpy(), P), b
+        assert np.array_equal(m.depth_estimator.seen[1][b].cpu().numpy(), E), b
+
+
+def test_record_pose_and_gt_pose(cuda):
+    B = 2
+    flow, K, pose = _batch(B, seed=12)
+    m = _model(flow, RECORD_POSE=True)
+    img = torch.zeros(B, 3, *HW, device=cuda)
+    P_mat, f = m(img, img, K)
+    assert P_mat.shape == (B, 1, 3, 4) and torch.equal(f.cpu(), flow)
+    m = _model(flow, GT_POSE_NORMALIZED=True)
+    flow_2D, P_mat, depth, _ = m(img, img, K, pose_gt=pose.to(cuda), use_gt_pose=True)
+    t = pose[:, :, 3]
+    assert torch.allclose(P_mat[:, 0, :, 3].cpu(), t / t.norm(dim=1, keepdim=True))
+    assert float(flow_2D.abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("mode", ["round", "sample_sp", "sift_pose"])
+def test_keypoint_points_match_oracle(cuda, mode):
+    from sfm_amd import ransac
+    B = 2
+    flow, K, _ = _batch(B, seed=13)
+    Ki = torch.inverse(K.float())
+    rng = np.random.default_rng(5)
+    kp1 = [rng.uniform(0, [HW[1] - 1, HW[0] - 1], (n, 2)) for n in (57, 33)]
+    kp1[0][:4] = [[0.5, 1.5], [2.5, 0.0], [HW[1] - 1.0, HW[0] - 1.0], [10.5, 20.5]]   # ties, corners
+    kp2 = [k + rng.normal(0, 2, k.shape) for k in kp1]
+    pts, n = ransac.keypoints_to_points(flow.to(cuda), Ki.to(cuda), kp1, kp2 if mode == "sift_pose" else None, mode)
+    assert n == [57, 33]
+    for b in range(B):
+        q, qp = OF.keypoint_correspondences(flow[b].numpy(), Ki[b].numpy(), kp1[b], kp2[b], mode)
+        got = pts[b, :n[b]].cpu().numpy()
+        want = np.c_[q, qp]
+        if mode == "sample_sp":
+            # CUDA-order unnormalisation ((x+1)/2)(W-1) vs torch-CPU's (x+1)((W-1)/2)
+            assert np.allclose(got, want, rtol=2e-6, atol=1e-7), np.abs(got - want).max()
+        else:
+            assert np.array_equal(got, want)
+
+
+def test_sparse_and_dense_pairs_in_one_batch(cuda):
+    B = 3
+    flow, K, _ = _batch(B, seed=14)
+    Ki = torch.inverse(K.float())
+    rng = np.random.default_rng(9)
+    kps = {0: rng.uniform(0, [HW[1] - 1, HW[0] - 1], (400, 2)), 1: rng.uniform(0, 50, (5, 2)),
+           2: rng.uniform(0, [HW[1] - 1, HW[0] - 1], (250, 2))}
+    calls = []
+
+    def matcher(r, t):
+        i = len(calls)
+        calls.append(r.shape)
+        return kps[i], kps[i] + 1.0
+
+    m = _model(flow, matcher=matcher)
+    img = torch.zeros(B, 3, *HW, device=cuda)
+    _, P_mat, _, _ = m(img, img, K)
+    assert len(calls) == B and calls[0] == (HW[0], HW[1], 3)
+    qd, qpd = OF.dense_correspondences(flow.numpy(), Ki.numpy())
+    for b in range(B):
+        if b == 1:          # 5 < min_matches: dense fallback (SFMnet.py:239-241)
+            q, qp = qd[b], qpd[b]
+        else:
+            q, qp = OF.keypoint_correspondences(flow[b].numpy(), Ki[b].numpy(), kps[b], mode="round")
+        _, P = _oracle_pose(q, qp, 2, 1e-4)
+        assert np.array_equal(P_mat[b, 0].cpu().numpy(), P), b
+
+
+def test_keypoint_index_errors(cuda):
+    from sfm_amd import ransac
+    flow, K, _ = _batch(1, seed=15)
+    Ki = torch.inverse(K.float()).to(cuda)
+    with pytest.raises(IndexError):
+        ransac.keypoints_to_points(flow.to(cuda), Ki, [np.array([[HW[1] - 0.4, 3.0]])])
+    # negative rounding wraps like torch indexing
+    pts, _ = ransac.keypoints_to_points(flow.to(cuda), Ki, [np.array([[-0.6, 3.0]])])
+    q, qp = OF.keypoint_correspondences(flow[0].numpy(), Ki[0].cpu().numpy(), np.array([[HW[1] - 1.0, 3.0]]))
+    assert np.array_equal(pts[0].cpu().numpy(), np.c_[q, qp])
