@@ -98,3 +98,38 @@ class CorrelationDepth(torch.nn.Module):
             pose[:, :, -1:] = pose[:, :, -1:] * self.norm_target
         cost = correlation_cost(ref_fea, tgt_fea, pose, K4, Ki4, self.nlabel, self.mindepth, self.predict_by_depth)
         return depth_head(cost, self.nlabel, self.mindepth, out_hw, self.predict_by_depth)
+
+
+class SweepDepthEstimator(torch.nn.Module):
+    """Drop-in ``depth_estimator`` for SFMnet with PSNet's call signature
+    (PSNet.forward(ref, targets, pose, intrinsics, intrinsics_inv, ...),
+    PSNet.py:128) and return value (depth_init, depth), parameter-free:
+    features = ``feature_fn(image)`` at quarter resolution (default: 4x4 average
+    pooling, matching PSNet's two stride-2 stages), the correlation cost over
+    the sweep planes averaged over target views (PSNet.py:166-170), and the
+    soft-argmin head at image resolution.  RESCALE_DEPTH scales pose[:, 0] in
+    place, as PSNet.py:135-136 does."""
+
+    def __init__(self, nlabel, mindepth=1.0, rescale_depth=False, norm_target=0.8, predict_by_depth=False,
+                 feature_fn=None):
+        super().__init__()
+        self.nlabel = int(nlabel)
+        self.mindepth = float(mindepth)
+        self.rescale_depth = rescale_depth
+        self.norm_target = norm_target
+        self.predict_by_depth = predict_by_depth
+        self.feature_fn = feature_fn or (lambda x: torch.nn.functional.avg_pool2d(x.float(), 4))
+
+    def forward(self, ref, targets, pose, intrinsics, intrinsics_inv, pose_gt=None, depth_gt=None, E_mat=None):
+        K4, Ki4 = quarter_intrinsics(intrinsics.float(), intrinsics_inv.float())
+        if self.rescale_depth:
+            pose[:, 0, :, -1:] = pose[:, 0, :, -1:] * self.norm_target
+        ref_fea = self.feature_fn(ref)
+        cost = None
+        for j, target in enumerate(targets):
+            c = correlation_cost(ref_fea, self.feature_fn(target), pose[:, j], K4, Ki4, self.nlabel, self.mindepth,
+                                 self.predict_by_depth)
+            cost = c if cost is None else cost + c
+        cost = cost / len(targets)
+        depth = depth_head(cost, self.nlabel, self.mindepth, (ref.shape[2], ref.shape[3]), self.predict_by_depth)
+        return depth, depth

@@ -141,3 +141,31 @@ def test_keypoint_index_errors(cuda):
     pts, _ = ransac.keypoints_to_points(flow.to(cuda), Ki, [np.array([[-0.6, 3.0]])])
     q, qp = OF.keypoint_correspondences(flow[0].numpy(), Ki[0].cpu().numpy(), np.array([[HW[1] - 1.0, 3.0]]))
     assert np.array_equal(pts[0].cpu().numpy(), np.c_[q, qp])
+
+
+def test_end_to_end_with_sweep_depth(cuda):
+    """SFMnet with only a flow estimator injected: RANSAC pose + correlation
+    sweep + soft-argmin head, checked against the oracle chain."""
+    from models.SFMnet import SFMnet
+    from sfm_amd.config import defaults
+    from sfm_amd.depth import SweepDepthEstimator
+    from oracle import sweep as S
+    B = 2
+    flow, K, _ = _batch(B, seed=16)
+    c = defaults()
+    c.update(ransac_iter=2, RESCALE_DEPTH=True, NORM_TARGET=0.6)
+    g = torch.Generator().manual_seed(3)
+    ref = torch.randn(B, 3, *HW, generator=g)
+    tgt = torch.randn(B, 3, *HW, generator=g)
+    m = SFMnet(32, 1.0, flow_estimator=_Flow(flow), cfg=c,
+               depth_estimator=SweepDepthEstimator(32, 1.0, rescale_depth=True, norm_target=0.6)).eval()
+    flow_2D, P_mat, depth, _ = m(ref.to(cuda), tgt.to(cuda), K)
+    assert depth.shape == (B, 1, *HW)
+    # oracle chain on the poses the model used (P_mat was rescaled in place, as PSNet does)
+    P = P_mat[:, 0].cpu()
+    Ki = torch.inverse(K.float())
+    f = lambda x: torch.nn.functional.avg_pool2d(x, 4)
+    cost = S.correlation_cost(f(ref), f(tgt), P, K, Ki, 32, 1.0)
+    want = S.depth_head(cost, 32, 1.0, HW)
+    rel = ((depth.cpu() - want).abs() / want.abs()).max()
+    assert float(rel) <= 1e-4, float(rel)
