@@ -305,7 +305,8 @@ __device__ __forceinline__ double to_vgpr(double s) {
 
 struct Addends { double e2, e5, e8, e6, e7; };
 
-template <bool FAST>
+// UNITM: every point of the chunk has M = 1 (mm2 = 1), so the guard is D >= Kg
+template <bool FAST, bool UNITM>
 __device__ __forceinline__ bool inlier_test(const double* E, const Addends& ad, double Kg, double x, double y,
                                             double xp, double yp, double mm2, const ScoreConsts& k) {
   if (!FAST) return inlier_reference(E, x, y, xp, yp, k.thr);
@@ -317,12 +318,43 @@ __device__ __forceinline__ bool inlier_test(const double* E, const Addends& ad, 
   const double a = fma(xp, ex0, fma(yp, ex1, ex2));
   const double D = fma(xe1, xe1, fma(xe0, xe0, fma(ex1, ex1, ex0 * ex0)));
   const double lhs = a * a;
-  const bool g = D >= Kg * mm2;
+  const bool g = UNITM ? (D >= Kg) : (D >= Kg * mm2);
   const bool fin = g && (lhs < k.t2lo * D);
   const bool fout = g && (lhs > k.t2hi * D);
   bool in = fin;
   if (!(fin || fout)) in = inlier_reference(E, x, y, xp, yp, k.thr);
   return in;
+}
+
+// One chunk (kPPL points per lane) against the tile's nc candidates.  One
+// ballot per (candidate, point); the num_test / num_ransac_test prefixes are
+// applied as precomputed wave masks (SAME: both prefixes equal, one count).
+template <bool FAST, bool UNITM, bool SAME>
+__device__ __forceinline__ void score_chunk(const double* __restrict__ CE, int nc, const double (&x)[kPPL],
+                                            const double (&y)[kPPL], const double (&xp)[kPPL],
+                                            const double (&yp)[kPPL], const double (&mm2)[kPPL],
+                                            const uint64_t (&mT)[kPPL], const uint64_t (&mR)[kPPL],
+                                            const ScoreConsts& kc, int lane, int32_t (*cnt)[2]) {
+  for (int c = 0; c < nc; ++c) {
+    double E[9];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) E[e] = CE[(size_t)c * kCandStride + e];
+    const double Kg = CE[(size_t)c * kCandStride + 9];
+    Addends ad;
+    if (FAST) ad = Addends{to_vgpr(E[2]), to_vgpr(E[5]), to_vgpr(E[8]), to_vgpr(E[6]), to_vgpr(E[7])};
+    int sT = 0, sR = 0;
+#pragma unroll
+    for (int k = 0; k < kPPL; ++k) {
+      const uint64_t m = __ballot(inlier_test<FAST, UNITM>(E, ad, Kg, x[k], y[k], xp[k], yp[k], mm2[k], kc));
+      sT += __popcll(m & mT[k]);
+      if (!SAME) sR += __popcll(m & mR[k]);
+    }
+    if (SAME) sR = sT;
+    if (lane == 0) {
+      cnt[c][0] += sT;
+      cnt[c][1] += sR;
+    }
+  }
 }
 
 template <bool FAST>
@@ -366,7 +398,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restric
     const double* CE = candE + ((size_t)b * cmax + c0) * kCandStride;
     for (int cb = p0; cb < p1; cb += kChunk) {
       double x[kPPL], y[kPPL], xp[kPPL], yp[kPPL], mm2[kPPL];
-      bool vT[kPPL], vR[kPPL];
+      uint64_t mT[kPPL], mR[kPPL];
+      bool unit = true;
 #pragma unroll
       for (int k = 0; k < kPPL; ++k) {
         const int p = cb + k * kScoreThreads + tid;
@@ -374,27 +407,17 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restric
         const double4 v = *reinterpret_cast<const double4*>(P + (size_t)(ok ? p : p0) * 4);
         x[k] = v.x; y[k] = v.y; xp[k] = v.z; yp[k] = v.w;
         mm2[k] = point_scale(v.x, v.y, v.z, v.w);
-        vT[k] = ok && p < T;
-        vR[k] = ok && p < R;
+        unit = unit && (mm2[k] == 1.0);
+        mT[k] = __ballot(ok && p < T);
+        mR[k] = __ballot(ok && p < R);
       }
-      for (int c = 0; c < nc; ++c) {
-        double E[9];
-#pragma unroll
-        for (int e = 0; e < 9; ++e) E[e] = CE[(size_t)c * kCandStride + e];
-        const double Kg = CE[(size_t)c * kCandStride + 9];
-        Addends ad;
-        if (FAST) ad = Addends{to_vgpr(E[2]), to_vgpr(E[5]), to_vgpr(E[8]), to_vgpr(E[6]), to_vgpr(E[7])};
-        int sT = 0, sR = 0;
-#pragma unroll
-        for (int k = 0; k < kPPL; ++k) {
-          const bool in = inlier_test<FAST>(E, ad, Kg, x[k], y[k], xp[k], yp[k], mm2[k], kc);
-          sT += __popcll(__ballot(in && vT[k]));
-          sR += __popcll(__ballot(in && vR[k]));
-        }
-        if (lane == 0) {
-          s_cnt[wv][c][0] += sT;
-          s_cnt[wv][c][1] += sR;
-        }
+      const bool all_unit = __all(unit);
+      if (T == R) {
+        if (all_unit) score_chunk<FAST, true, true>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
+        else score_chunk<FAST, false, true>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
+      } else {
+        if (all_unit) score_chunk<FAST, true, false>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
+        else score_chunk<FAST, false, false>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
       }
     }
     __syncthreads();
