@@ -15,6 +15,7 @@ struct Tuning {
   int sweep_items_per_block = 4; // consecutive (row, plane, window) items per sweep block
   int sweep_lane_pixels = 0;     // 1: warped lanes own 4 consecutive pixels (16-byte stores)
   int score_blocks_per_cu = 32;  // persistent score grid
+  int score_fp32 = 1;            // packed float32 pre-decision in the score kernel
 };
 Tuning& tuning();
 

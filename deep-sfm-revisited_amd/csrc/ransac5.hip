@@ -32,7 +32,7 @@ namespace sfm {
 
 constexpr int kChains = SFM_RANSAC_CHAINS;
 constexpr int kMaxSlots = 10;
-constexpr int kCandStride = 12;   // doubles per candidate E (9 used), 96 B
+constexpr int kCandStride = 18;   // per candidate: E f64[9], Kg, then float[14] (E f32[9], A1, B1, A2, B2, ok32)
 constexpr int kKC = 32;           // candidates per score tile
 constexpr int kPPL = 8;           // points per lane per chunk
 constexpr int kScoreThreads = 256;
@@ -182,6 +182,45 @@ __device__ __forceinline__ double guard_constant(const double* E, double g) {
 }
 
 // ---------------------------------------------------------------------------
+// Float32 pre-decision (k_score32).  With u = 2^-24, M = max(1, |x|, |y|,
+// |x'|, |y'|) <= 2^12 and R = sum|E_ij| in [2^-30, 2^30], the float32 FMA
+// evaluation (inputs rounded to float32) satisfies
+//     |a_s - a*| <= alpha = 8 u R M^2,   ||v_s - v*|| <= beta = 8.1 u R M
+// against the exact values a*, v* of the float64 inputs (7.1 u R M^2 and
+// 8.02 u R M by the standard bounds; the reference's own float64 error is far
+// below the slack).  Bounding the cross terms 2|a|alpha and 2 sqrt(D) beta by
+// AM-GM with weight 2^7 turns the reference test into two sign tests:
+//     inlier  if fma(-t2lo, D, fma(a, a,  eps1)) < 0
+//     outlier if fma(-t2hi, D, fma(a, a, -eps2)) > 0
+//     eps1 = 129 alpha^2 + 128 thr^2 beta^2           = A1 M^4 + B1 M^2
+//     eps2 = (128 alpha^2 + 129 thr^2 beta^2)/(1-2^-7) = A2 M^4 + B2 M^2
+//     t2lo = thr^2 (1 - 2^-6 - 2^-19),  t2hi = thr^2 (1 + 2^-7)/(1 - 2^-7) (1 + 2^-19)
+// (derivation in DESIGN.md, "Scoring").  Anything else is undecided and
+// re-evaluated by the float64 path.  A*, B* carry a 2^-20 upward slack that
+// covers their float32 rounding and the three float32 operations forming eps.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fp32_constants(const double* E, double thr, bool enable, float* out) {
+  double R = 0.0;
+  bool finite = true;
+#pragma unroll
+  for (int e = 0; e < 9; ++e) {
+    R += fabs(E[e]);
+    finite = finite && isfinite(E[e]);
+  }
+  const bool ok = enable && finite && R >= 0x1p-30 && R <= 0x1p30;
+#pragma unroll
+  for (int e = 0; e < 9; ++e) out[e] = ok ? (float)E[e] : 0.0f;
+  const double al = 8.0 * 0x1p-24 * R * (1.0 + 0x1p-20) + 0x1p-120;
+  const double be = 8.1 * 0x1p-24 * R * (1.0 + 0x1p-20) + 0x1p-120;
+  const double t2 = thr * thr, up = 1.0 + 0x1p-20;
+  out[9] = ok ? (float)(129.0 * al * al * up) : 0.0f;
+  out[10] = ok ? (float)(128.0 * t2 * be * be * up) : 0.0f;
+  out[11] = ok ? (float)(128.0 * al * al / (1.0 - 0x1p-7) * up) : 0.0f;
+  out[12] = ok ? (float)(129.0 * t2 * be * be / (1.0 - 0x1p-7) * up) : 0.0f;
+  out[13] = ok ? 1.0f : 0.0f;
+}
+
+// ---------------------------------------------------------------------------
 // Phase 2: chains and the dense candidate list (one block of 512 per pair)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
@@ -192,7 +231,8 @@ __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
                                                    double* __restrict__ hypP0,
                                                    int32_t* __restrict__ cand_off,
                                                    int32_t* __restrict__ cand_total,
-                                                   double* __restrict__ candE, int cmax, double guard_g) {
+                                                   double* __restrict__ candE, int cmax, double guard_g,
+                                                   double thr, int fast32) {
   __shared__ int32_t s_sum[kChains / 64];
   const int b = blockIdx.x, t = threadIdx.x;
   const size_t hb0 = (size_t)b * H;
@@ -234,6 +274,7 @@ __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
 #pragma unroll
         for (int e = 0; e < 9; ++e) dst[e] = Eh[j * 9 + e];
         dst[9] = guard_constant(dst, guard_g);
+        fp32_constants(dst, thr, fast32 != 0, reinterpret_cast<float*>(dst + 10));
       }
       off += nc;
     } else {
@@ -242,6 +283,7 @@ __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
 #pragma unroll
       for (int e = 0; e < 9; ++e) dst[e] = nr > 0 ? Eh[e] : E0[e];
       dst[9] = guard_constant(dst, guard_g);
+      fp32_constants(dst, thr, fast32 != 0, reinterpret_cast<float*>(dst + 10));
 #pragma unroll
       for (int e = 0; e < 12; ++e) hypP0[hb * 12 + e] = P0[e];
       off += 1;
@@ -263,6 +305,8 @@ __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
 // ---------------------------------------------------------------------------
 struct ScoreConsts {
   double thr, t2lo, t2hi;
+  float t2lo32, t2hi32;
+  int fast32;
 };
 
 // Exact reference evaluation (ComputeError, kernel_functions.cu:232-264).
@@ -418,6 +462,266 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restric
       } else {
         if (all_unit) score_chunk<FAST, true, false>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
         else score_chunk<FAST, false, false>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
+      }
+    }
+    __syncthreads();
+    if (tid < nc * 2) {
+      const int c = tid >> 1, which = tid & 1;
+      int s = 0;
+#pragma unroll
+      for (int w = 0; w < kScoreThreads / 64; ++w) { s += s_cnt[w][c][which]; s_cnt[w][c][which] = 0; }
+      if (s) atomicAdd((which ? cntR : cntT) + (size_t)b * cmax + c0 + c, s);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase 3b: scoring with the float32 pre-decision (fp32_constants).
+// Same work decomposition as k_score; only float32 copies of the points stay
+// in registers.  (Plain v_fma_f32 issues at twice the fp64 rate on gfx950;
+// packed v_pk_fma_f32 measured no faster.)  Undecided lanes and the rare
+// chunks with a coordinate beyond +-1 reload their points and take the
+// float64 test.
+// ---------------------------------------------------------------------------
+
+// wave-uniform pointer kept in SGPRs (the compiler cannot prove uniformity of
+// values derived from the LDS pair search)
+template <typename Tp>
+__device__ __forceinline__ const Tp* uniform_ptr(const Tp* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const Tp*>(((uint64_t)hi << 32) | lo);
+}
+
+#ifdef SFM_SCORE_STATS
+// experiment builds only (scripts/score_experiment.py): pair-iterations,
+// pair-iterations with an undecided lane, undecided lane-evaluations
+__device__ unsigned long long g_score_stats[3];
+extern "C" int sfm_experiment_score_stats(unsigned long long* out3) {
+  return hipMemcpyFromSymbol(out3, HIP_SYMBOL(g_score_stats), 24) == hipSuccess ? 0 : 2;
+}
+#endif
+
+// float64 decision of one point (reloaded); guard per point (any scale)
+__device__ __forceinline__ bool inlier_f64(const double* __restrict__ Ec, const double* __restrict__ P, int p,
+                                           const ScoreConsts& kc) {
+  const double4 v = *reinterpret_cast<const double4*>(P + (size_t)p * 4);
+  double E[9];
+#pragma unroll
+  for (int e = 0; e < 9; ++e) E[e] = Ec[e];
+  const Addends ad{E[2], E[5], E[8], E[6], E[7]};
+  return inlier_test<true, false>(E, ad, Ec[9], v.x, v.y, v.z, v.w, point_scale(v.x, v.y, v.z, v.w), kc);
+}
+
+// Float32 pass of one chunk.  Every decision is a wave mask straight out
+// of one compare (inlier: din < 0, outlier: dout > 0; both finite here since
+// the chunk's coordinates are within +-1 and the candidate passed ok32), so
+// the bookkeeping is scalar: counts by popcount, undecided = ~(in | out) per
+// point.  Undecided points are re-tested in float64 after the unrolled loop.
+constexpr int kQueue = 1024;   // undecided (candidate, point) entries per wave (LDS)
+
+template <bool SAME, bool MASKED>
+__device__ __forceinline__ void score32_chunk(const double* __restrict__ CE, int nc, const double* __restrict__ P,
+                                              int cb, int tid, int p1, int T, int R, const float (&x)[kPPL],
+                                              const float (&y)[kPPL], const float (&xp)[kPPL],
+                                              const float (&yp)[kPPL], const uint64_t (&mT)[kPPL],
+                                              const uint64_t (&mR)[kPPL], float M2, uint64_t bad,
+                                              const ScoreConsts& kc, int lane, int32_t (*cnt)[2], uint32_t* q) {
+  const float nt2lo = -kc.t2lo32, nt2hi = -kc.t2hi32;
+  const float M4 = M2 * M2;
+  int qn = 0;
+  for (int c = 0; c < nc; ++c) {
+    const double* Ec = CE + (size_t)c * kCandStride;     // the tile's records, staged in LDS
+    const float* F = reinterpret_cast<const float*>(Ec + 10);
+    int sT = 0, sR = 0;
+    uint64_t und[kPPL];
+    if (F[13] != 0.0f) {
+      const float e0 = F[0], e1 = F[1], e2 = F[2], e3 = F[3], e4 = F[4], e5 = F[5], e6 = F[6], e7 = F[7], e8 = F[8];
+      const float eps1 = __builtin_fmaf(F[9], M4, F[10] * M2);      // per lane: its points' M
+      const float neps2 = -__builtin_fmaf(F[11], M4, F[12] * M2);
+      // stage by stage across the kPPL points: independent FMA chains
+      float ex0[kPPL], ex1[kPPL], ex2[kPPL], xe0[kPPL], xe1[kPPL], a[kPPL], D[kPPL], din[kPPL], dout[kPPL];
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) ex0[k] = __builtin_fmaf(e0, x[k], __builtin_fmaf(e1, y[k], e2));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) ex1[k] = __builtin_fmaf(e3, x[k], __builtin_fmaf(e4, y[k], e5));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) ex2[k] = __builtin_fmaf(e6, x[k], __builtin_fmaf(e7, y[k], e8));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) xe0[k] = __builtin_fmaf(xp[k], e0, __builtin_fmaf(yp[k], e3, e6));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) xe1[k] = __builtin_fmaf(xp[k], e1, __builtin_fmaf(yp[k], e4, e7));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) a[k] = __builtin_fmaf(xp[k], ex0[k], __builtin_fmaf(yp[k], ex1[k], ex2[k]));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k)
+        D[k] = __builtin_fmaf(xe1[k], xe1[k], __builtin_fmaf(xe0[k], xe0[k], __builtin_fmaf(ex1[k], ex1[k], ex0[k] * ex0[k])));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) din[k] = __builtin_fmaf(nt2lo, D[k], __builtin_fmaf(a[k], a[k], eps1));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) dout[k] = __builtin_fmaf(nt2hi, D[k], __builtin_fmaf(a[k], a[k], neps2));
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) {
+        const uint64_t mi = __ballot(din[k] < 0.0f) & ~bad;
+        const uint64_t mo = __ballot(dout[k] > 0.0f);
+        und[k] = ~(mi | mo) | bad;
+        if (MASKED) {
+          und[k] &= mT[k] | mR[k];
+          sT += __popcll(mi & mT[k]);
+          if (!SAME) sR += __popcll(mi & mR[k]);
+        } else {
+          sT += __popcll(mi);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) und[k] = MASKED ? (mT[k] | mR[k]) : ~0ull;   // candidate outside the float32 range
+    }
+#ifdef SFM_SCORE_STATS
+    {
+      uint64_t any = 0;
+      int n = 0;
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) { any |= und[k]; n += __popcll(und[k]); }
+      if (lane == 0) {
+        atomicAdd(&g_score_stats[0], 1ull);
+        if (any) atomicAdd(&g_score_stats[1], 1ull);
+        atomicAdd(&g_score_stats[2], (unsigned long long)n);
+      }
+    }
+#endif
+#ifndef SFM_SCORE_NOFALLBACK
+    int nund = 0;
+#pragma unroll
+    for (int k = 0; k < kPPL; ++k) nund += __popcll(und[k]);
+    if (nund) {
+      if (qn + nund <= kQueue) {
+        // queue (candidate, point) for the compacted float64 pass after the loop
+#pragma unroll
+        for (int k = 0; k < kPPL; ++k) {
+          if (!und[k]) continue;                          // wave-uniform
+          if ((und[k] >> lane) & 1ull) {
+            const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(und[k] >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)und[k], 0));
+            q[pos] = ((uint32_t)c << 24) | (uint32_t)(cb + k * kScoreThreads + tid);
+          }
+          qn += __popcll(und[k]);
+        }
+      } else {
+        // queue full: float64 test now, one point per lane per round
+#pragma unroll 1
+        for (int k = 0; k < kPPL; ++k) {
+          if (!und[k]) continue;
+          const int p = cb + k * kScoreThreads + tid;
+          bool in = false;
+          if ((und[k] >> lane) & 1ull) in = inlier_f64(Ec, P, p, kc);
+          const uint64_t m = __ballot(in);
+          if (MASKED) {
+            sT += __popcll(m & mT[k]);
+            if (!SAME) sR += __popcll(m & mR[k]);
+          } else {
+            sT += __popcll(m);
+          }
+        }
+      }
+    }
+#endif
+    if (SAME || !MASKED) sR = sT;
+    if (lane == 0) {
+      cnt[c][0] += sT;
+      cnt[c][1] += sR;
+    }
+  }
+  // compacted float64 pass over the queued evaluations (64 per round)
+#pragma unroll 1
+  for (int i = lane; i < qn; i += 64) {
+    const uint32_t e = q[i];
+    const int c = (int)(e >> 24), p = (int)(e & 0xffffffu);
+    if (inlier_f64(CE + (size_t)c * kCandStride, P, p, kc)) {
+      if (p < T) atomicAdd(&cnt[c][0], 1);
+      if (p < R) atomicAdd(&cnt[c][1], 1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kScoreThreads) void k_score32(const double* __restrict__ pts, int64_t n_stride,
+                                                           PairParams pp, int batch, int cmax,
+                                                           const int32_t* __restrict__ cand_total,
+                                                           const double* __restrict__ candE,
+                                                           int32_t* __restrict__ cntT, int32_t* __restrict__ cntR,
+                                                           ScoreConsts kc) {
+  __shared__ int32_t s_cnt[kScoreThreads / 64][kKC][2];
+  __shared__ int32_t s_items[SFM_MAX_BATCH + 1];
+  __shared__ int32_t s_tiles[SFM_MAX_BATCH];
+  __shared__ double s_cand[kKC * kCandStride];
+  __shared__ uint32_t s_queue[kScoreThreads / 64][kQueue];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) {
+    int acc = 0;
+    for (int b = 0; b < batch; ++b) {
+      const int tiles = (cand_total[b] + kKC - 1) / kKC;
+      s_tiles[b] = tiles;
+      s_items[b] = acc;
+      acc += tiles * pp.splits[b];
+    }
+    s_items[batch] = acc;
+  }
+  for (int i = tid; i < (kScoreThreads / 64) * kKC * 2; i += kScoreThreads) (&s_cnt[0][0][0])[i] = 0;
+  __syncthreads();
+  const int total = __builtin_amdgcn_readfirstlane(s_items[batch]);
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    int b = 0;
+    while (item >= s_items[b + 1]) ++b;
+    b = __builtin_amdgcn_readfirstlane(b);                      // wave-uniform (LDS-derived)
+    const int tiles = __builtin_amdgcn_readfirstlane(s_tiles[b]);
+    const int local = item - __builtin_amdgcn_readfirstlane(s_items[b]);
+    const int split = local / tiles, tile = local - split * tiles;
+    const int ctot = cand_total[b];
+    const int c0 = tile * kKC;
+    const int nc = min(kKC, ctot - c0);
+    const int T = pp.test[b], R = pp.rtest[b];
+    const int M = max(T, R);
+    const int p0 = split * kPtsPerItem;
+    const int p1 = min(M, p0 + kPtsPerItem);
+    const double* P = pts + (size_t)b * n_stride * 4;
+    {
+      // stage the tile's candidate records (nc x 128 B) in LDS
+      const double2* src = reinterpret_cast<const double2*>(candE + ((size_t)b * cmax + c0) * kCandStride);
+      double2* dst = reinterpret_cast<double2*>(s_cand);
+      for (int i = tid; i < nc * (kCandStride / 2); i += kScoreThreads) dst[i] = src[i];
+    }
+    __syncthreads();
+    const double* CE = s_cand;
+    for (int cb = p0; cb < p1; cb += kChunk) {
+      float x[kPPL], y[kPPL], xp[kPPL], yp[kPPL];
+      uint64_t mT[kPPL], mR[kPPL];
+      double M = 1.0;
+#pragma unroll
+      for (int k = 0; k < kPPL; ++k) {
+        const int p = cb + k * kScoreThreads + tid;
+        const double4 v = *reinterpret_cast<const double4*>(P + (size_t)min(p, p1 - 1) * 4);
+        M = fmax(M, fmax(fmax(fabs(v.x), fabs(v.y)), fmax(fabs(v.z), fabs(v.w))));
+        x[k] = (float)v.x; y[k] = (float)v.y; xp[k] = (float)v.z; yp[k] = (float)v.w;
+        mT[k] = __ballot(p < p1 && p < T);
+        mR[k] = __ballot(p < p1 && p < R);
+      }
+      // lanes with a coordinate beyond 2^12 (or NaN) take the float64 test for all their points
+      const bool lane_bad = !(M <= 0x1p12);
+      const uint64_t bad = __ballot(lane_bad);
+      const float Mf = lane_bad ? 1.0f : (float)M;
+      const float M2 = Mf * Mf;
+      const bool full = cb + kChunk <= min(T, R);                 // no prefix masking needed
+      if (full) {
+        score32_chunk<true, false>(CE, nc, P, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
+                                   s_cnt[wv], s_queue[wv]);
+      } else if (T == R) {
+        score32_chunk<true, true>(CE, nc, P, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
+                                  s_cnt[wv], s_queue[wv]);
+      } else {
+        score32_chunk<false, true>(CE, nc, P, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
+                                   s_cnt[wv], s_queue[wv]);
       }
     }
     __syncthreads();
@@ -647,21 +951,32 @@ static int run_chunk(const double* pts, int64_t n_stride, const int64_t* n, int 
   SFM_LAUNCHED();
   const bool fast = thr >= 0x1p-40 && thr < 1.0;
   const double guard_g = fast ? 0x1p24 * (11.0 + 11.0 / thr) : 0.0;
+  const bool fast32 = fast && thr >= 0x1p-20 && tuning().score_fp32;
   {
     ProfScope ps("ransac_chain", s);
     hipLaunchKernelGGL(k_chain, dim3(bc), dim3(kChains), 0, s, H, iters, cheir, w.nroots, w.ncand, w.hypE,
-                       w.hypP, w.hypP0, w.cand_off, w.cand_total, w.candE, cmax, guard_g);
+                       w.hypP, w.hypP0, w.cand_off, w.cand_total, w.candE, cmax, guard_g, thr, fast32 ? 1 : 0);
   }
   SFM_LAUNCHED();
   SFM_HIP(hipMemsetAsync(w.cntT, 0, (size_t)bc * cmax * 4, s));
   SFM_HIP(hipMemsetAsync(w.cntR, 0, (size_t)bc * cmax * 4, s));
-  ScoreConsts kc{thr, (thr * thr) * (1.0 - 0x1p-22), (thr * thr) * (1.0 + 0x1p-22)};
+  ScoreConsts kc;
+  kc.thr = thr;
+  kc.t2lo = (thr * thr) * (1.0 - 0x1p-22);
+  kc.t2hi = (thr * thr) * (1.0 + 0x1p-22);
+  // float32 thresholds with directed slack (see fp32_constants)
+  kc.t2lo32 = (float)((thr * thr) * (1.0 - 0x1p-6 - 0x1p-19));
+  kc.t2hi32 = (float)((thr * thr) * (1.0 + 0x1p-7) / (1.0 - 0x1p-7) * (1.0 + 0x1p-19));
+  kc.fast32 = fast32 ? 1 : 0;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = std::max(1, cus) * tuning().score_blocks_per_cu;
   {
     ProfScope ps("ransac_score", s);
-    if (fast)
+    if (fast32)
+      hipLaunchKernelGGL(k_score32, dim3(grid), dim3(kScoreThreads), 0, s, pts, n_stride, pp, bc, cmax,
+                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
+    else if (fast)
       hipLaunchKernelGGL(k_score<true>, dim3(grid), dim3(kScoreThreads), 0, s, pts, n_stride, pp, bc, cmax,
                          w.cand_total, w.candE, w.cntT, w.cntR, kc);
     else

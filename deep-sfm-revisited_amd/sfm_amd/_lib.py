@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsfm_hip.so")
+LIB_PATH = os.environ.get("SFM_HIP_LIB") or os.path.join(_HERE, "libsfm_hip.so")   # override: A/B of library builds
 
 _c_dp = ctypes.c_void_p
 _i64p = ctypes.POINTER(ctypes.c_int64)

@@ -156,3 +156,26 @@ def test_fast_path_guard_near_epipole(cuda, thr, scale):
     ref = R.ransac5(q, qp, n, n, 2, thr)
     assert r["winner"] == ref["winner"] and r["inliers"] == ref["inliers"]
     assert np.array_equal(r["scores"], ref["hyp_score"])
+
+
+def test_fp32_predecision_is_exact(cuda):
+    """The packed-fp32 pre-decision of the score kernel must not change any
+    count: per-hypothesis scores with it on and off are identical (and equal
+    the oracle's on a dense synthetic pair)."""
+    from sfm_amd import _lib, ransac, synth
+    from oracle import ransac5 as ORR
+    flow, K, _, _ = synth.kitti_pair_batch(2, seed=77, hw=(120, 200))
+    Ki = torch.inverse(K.float())
+    pts = ransac.flow_to_points(flow.to(cuda), Ki.to(cuda))
+    outs = []
+    for flag in (1, 0):
+        _lib.tune("score_fp32", flag)
+        try:
+            outs.append(ransac.ransac5_batched(pts, iters=2, threshold=1e-4, return_scores=True))
+        finally:
+            _lib.tune("score_fp32", 1)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    p = pts[0].cpu().numpy()
+    r = ORR.ransac5(p[:, :2], p[:, 2:], iters=2, thr=1e-4)
+    assert np.array_equal(outs[0][4][0].cpu().numpy(), r["hyp_score"])
