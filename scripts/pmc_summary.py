@@ -17,14 +17,14 @@ import json
 import os
 import sys
 
-KERNELS = {"k_score": "ransac_score", "k_sweep": "plane_sweep", "k_solve": "ransac_solve",
+KERNELS = {"k_score32": "ransac_score", "k_score": "ransac_score", "k_sweep": "plane_sweep", "k_solve": "ransac_solve",
            "k_chain": "ransac_chain", "k_tgt_quads": "sweep_tgt_quads", "k_flow_points": "flow_to_points"}
 
 
 def kernel_key(name):
     base = name.split("(")[0]
-    for k, v in KERNELS.items():
-        if base.endswith(k) or ("::" + k + "<") in base:
+    for k, v in KERNELS.items():     # k_score32 is checked before k_score
+        if base.endswith("::" + k) or ("::" + k + "<") in base:
             return v
     return None
 
