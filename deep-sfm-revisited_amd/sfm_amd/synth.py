@@ -67,11 +67,16 @@ def rigid_flow(depth, pose, K):
     return flow, behind
 
 
-def kitti_pair_batch(batch, seed=0, hw=KITTI_HW, noise_px=0.5, outlier_frac=0.15, device="cpu"):
-    """Synthetic (flow [B,2,H,W] f32, K [B,3,3] f32, pose_gt [B,3,4] f32, depth [B,H,W] f32)."""
+INDOOR_K = (518.86, 519.47, 325.58, 253.74)   # 640x480 (NYU/ScanNet-like; DeMoN-style indoor pairs)
+INDOOR_HW = (480, 640)
+
+
+def kitti_pair_batch(batch, seed=0, hw=KITTI_HW, noise_px=0.5, outlier_frac=0.15, device="cpu", k=None):
+    """Synthetic (flow [B,2,H,W] f32, K [B,3,3] f32, pose_gt [B,3,4] f32, depth [B,H,W] f32).
+    ``k`` = (fx, fy, cx, cy) (default: KITTI)."""
     gen = torch.Generator().manual_seed(int(seed))
     H, W = hw
-    K = intrinsics(batch)
+    K = intrinsics(batch) if k is None else intrinsics(batch, *k)
     pose = relative_pose(batch, gen)
     depth = depth_field(batch, H, W, gen)
     flow, behind = rigid_flow(depth, pose, K)
