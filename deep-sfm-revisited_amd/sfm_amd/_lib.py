@@ -50,6 +50,10 @@ _SIGS = [
     ("sfm_keypoints_to_points", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, ctypes.c_int64,
       _c_dp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_int64, _c_dp]),
+    ("sfm_essential_optimise_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int64]),
+    ("sfm_essential_optimise_batched", ctypes.c_int,
+     [_c_dp, ctypes.c_int64, _c_dp, ctypes.c_int, _c_dp, ctypes.c_double, ctypes.c_double, ctypes.c_int, _c_dp,
+      _c_dp, ctypes.c_size_t, _c_dp]),
     ("sfm_correlation_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("sfm_plane_sweep_correlation", ctypes.c_int,
      [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,

@@ -209,3 +209,25 @@ def keypoints_to_points(flow, intrinsic_inv, kp1, kp2=None, mode="round", h_side
             nmax, _lib.i64_array(n), m, _lib.ptr(Ki), _lib.ptr(out), out.shape[1], _lib.stream_ptr(dev)),
             "sfm_keypoints_to_points")
     return out, n
+
+
+def optimise_batched(pts, E_init, delta=0.001, alpha=0.0, max_reps=200, n=None, workspace=None):
+    """GPU IRLS refinement of E for a batch of pairs (the loop of
+    EssentialMatrixOptimise, polish_E.cu:1470-1577): pts [B, N, 4] float64,
+    E_init [B, 3, 3] float64 (CUDA) -> E [B, 3, 3].  Agrees with the host
+    `essential_matrix.optimise` to rounding level (reassociated sums)."""
+    _check_dev_f64(pts, "pts")
+    B, ns, _ = pts.shape
+    n = [ns] * B if n is None else [int(v) for v in n]
+    E0 = E_init.reshape(B, 9).to(pts.device, torch.float64).contiguous()
+    out = torch.empty(B, 3, 3, dtype=torch.float64, device=pts.device)
+    L = _lib.load()
+    with torch.cuda.device(pts.device):
+        if workspace is None:
+            nb = L.sfm_essential_optimise_workspace_bytes(B, ns)
+            workspace = torch.empty(int(nb), dtype=torch.uint8, device=pts.device)
+        rc = L.sfm_essential_optimise_batched(_lib.ptr(pts), ns, _lib.i64_array(n), B, _lib.ptr(E0), float(delta),
+                                              float(alpha), int(max_reps), _lib.ptr(out), _lib.ptr(workspace),
+                                              workspace.numel(), _lib.stream_ptr(pts.device))
+        _lib.check(rc, "sfm_essential_optimise_batched")
+    return out

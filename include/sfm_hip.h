@@ -147,6 +147,15 @@ int sfm_pack_points(const double* q, const double* qp, int64_t n, double* pts_ou
  * 76-105, polish_E.cu:1470-1577).  All pointers [host]; q, qp n x 2. */
 int sfm_essential_optimise(const double* q, const double* qp, int64_t n, const double* E_init,
                            double delta, double alpha, int max_reps, double* E_out);
+/* Batched GPU form of the same IRLS.  The sums are
+ * reassociated (parallel reduction), so E agrees with the host version to
+ * rounding level, not bit for bit.
+ *   pts [dev] batch x n_stride x 4 float64 (x, y, x', y'); n [host] batch;
+ *   E_init, E_out [dev] batch x 9 float64. */
+size_t sfm_essential_optimise_workspace_bytes(int batch, int64_t n_max);
+int sfm_essential_optimise_batched(const double* pts, int64_t n_stride, const int64_t* n, int batch,
+                                   const double* E_init, double delta, double alpha, int max_reps,
+                                   double* E_out, void* workspace, size_t workspace_bytes, void* stream);
 /* EssentialMatrixDecompose -> Edecomp(E, params) (essential_matrix.cu:29-43). */
 int sfm_essential_decompose(const double* E, double* params5);
 /* EssentialMatrixDecomposeUV -> Edecomp(E, U, V) (essential_matrix.cu:48-70). */

@@ -8,5 +8,5 @@ mkdir -p ../../scripts/exp
 for v in STATS NOFALLBACK; do
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -fPIC -shared \
         -I../../include -Wno-unused-result -DSFM_SCORE_$v -o ../../scripts/exp/libsfm_hip_$v.so \
-        capi.hip ransac5.hip sweep.hip depth.hip host_polish.cpp
+        capi.hip ransac5.hip sweep.hip depth.hip irls.hip host_polish.cpp
 done

@@ -102,3 +102,20 @@ def test_c3_batch32_and_bf16(cuda):
     f32 = plane_sweep_cost(*args)
     b16 = plane_sweep_cost(*args, dtype=torch.bfloat16)
     assert torch.equal(b16.cpu(), f32.to(torch.bfloat16).cpu())
+
+
+@pytest.mark.parametrize("delta,alpha,reps", [(1e-3, 0.0, 200), (2e-3, 1.0, 30), (1e-3, 0.5, 0)])
+def test_gpu_irls_matches_host(cuda, delta, alpha, reps):
+    """GPU IRLS (sfm_essential_optimise_batched) vs the host restatement of
+    polish_E_robust_parametric: 1e-4 relative on E (reassociated sums)."""
+    from sfm_amd import ransac, synth
+    B = 3
+    flow, K, _, _ = synth.kitti_pair_batch(B, seed=31, hw=(120, 200))
+    pts = _pts(flow, K, cuda)
+    E, _, _, _ = ransac.ransac5_batched(pts, iters=1, threshold=1e-4)
+    got = ransac.optimise_batched(pts, E, delta, alpha, reps).cpu().numpy()
+    for b in range(B):
+        p = pts[b].cpu().numpy()
+        want = R.optimise(p[:, :2], p[:, 2:], E[b].cpu().numpy(), delta, alpha, reps)
+        rel = np.abs(got[b] - want).max() / np.abs(want).max()
+        assert rel <= 1e-4, (b, rel)
