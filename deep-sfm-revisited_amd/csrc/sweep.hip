@@ -101,7 +101,13 @@ struct SweepGeom {
 };
 
 // one warped item: 4 channels of the window at plane l
-template <typename OutT, bool VEC, bool LANE_PIX>
+template <typename OutT> __device__ __forceinline__ void store1_nt(OutT* dst, float v);
+template <> __device__ __forceinline__ void store1_nt<float>(float* dst, float v) { __builtin_nontemporal_store(v, dst); }
+template <> __device__ __forceinline__ void store1_nt<unsigned short>(unsigned short* dst, float v) {
+  __builtin_nontemporal_store(to_bf16(v), dst);
+}
+
+template <typename OutT, bool VEC, bool LANE_PIX, bool NT = false>
 __device__ __forceinline__ void warp_quad(const f32x4* __restrict__ tq, const float* __restrict__ pose,
                                           const float* __restrict__ K4, const float* __restrict__ K4inv,
                                           const SweepGeom& g, int b, int q, int l, int p0, OutT* plane,
@@ -153,7 +159,10 @@ __device__ __forceinline__ void warp_quad(const f32x4* __restrict__ tq, const fl
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int pj = wave_base + 64 * j + lane;
-        if (pj >= 0 && pj < hw) store1(row + pj, acc[j][k]);
+        if (pj >= 0 && pj < hw) {
+          if (NT) store1_nt(row + pj, acc[j][k]);
+          else store1(row + pj, acc[j][k]);
+        }
       }
     }
   }
@@ -198,7 +207,7 @@ struct ItemPos {
   }
 };
 
-template <typename OutT, bool VEC, int IPB, bool LANE_PIX = true>
+template <typename OutT, bool VEC, int IPB, bool LANE_PIX = true, bool NT = false>
 __global__ __launch_bounds__(kSwThreads) void k_sweep(const float* __restrict__ ref, const f32x4* __restrict__ tq,
                                                       const float* __restrict__ pose, const float* __restrict__ K4,
                                                       const float* __restrict__ K4inv, SweepGeom g,
@@ -242,7 +251,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep(const float* __restrict__ 
       load_ref4(ref, ((size_t)ip.b * g.C + ip.grp) * hw, p0, hw, v);
       store_row<OutT, VEC>(plane + (size_t)ip.grp * rstride, p0, hw, v);
     } else {
-      warp_quad<OutT, VEC, LANE_PIX>(tq, pose, K4, K4inv, g, ip.b, ip.grp - g.ref_rows, ip.l, p0, plane, rstride);
+      warp_quad<OutT, VEC, LANE_PIX, NT>(tq, pose, K4, K4inv, g, ip.b, ip.grp - g.ref_rows, ip.l, p0, plane, rstride);
     }
   }
 }
@@ -284,23 +293,27 @@ __global__ __launch_bounds__(kSweepThreads) void k_inverse_warp(const float* __r
   }
 }
 
-template <typename OutT, bool VEC, bool LP>
+template <typename OutT, bool VEC, bool LP, bool NT>
 static void launch_k_sweep_lp(int ipb, int64_t blocks, hipStream_t s, const float* ref, const f32x4* tq, const float* pose,
                            const float* K4, const float* K4inv, const SweepGeom& g, void* out) {
   const dim3 grid((unsigned)blocks), block(kSwThreads);
   switch (ipb) {
-    case 1: hipLaunchKernelGGL((k_sweep<OutT, VEC, 1, LP>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
-    case 2: hipLaunchKernelGGL((k_sweep<OutT, VEC, 2, LP>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
-    case 4: hipLaunchKernelGGL((k_sweep<OutT, VEC, 4, LP>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
-    default: hipLaunchKernelGGL((k_sweep<OutT, VEC, 8, LP>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
+    case 1: hipLaunchKernelGGL((k_sweep<OutT, VEC, 1, LP, NT>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
+    case 2: hipLaunchKernelGGL((k_sweep<OutT, VEC, 2, LP, NT>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
+    case 4: hipLaunchKernelGGL((k_sweep<OutT, VEC, 4, LP, NT>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out); break;
+    default: hipLaunchKernelGGL((k_sweep<OutT, VEC, 8, LP, NT>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
   }
 }
 
 template <typename OutT, bool VEC>
 static void launch_k_sweep(int ipb, int64_t blocks, hipStream_t s, const float* ref, const f32x4* tq, const float* pose,
                            const float* K4, const float* K4inv, const SweepGeom& g, void* out) {
-  if (tuning().sweep_lane_pixels) launch_k_sweep_lp<OutT, VEC, true>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
-  else launch_k_sweep_lp<OutT, VEC, false>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+  // sweep_lane_pixels: 0 lane-consecutive pixels (default), 1 four pixels per
+  // lane (16-byte stores), 2 lane-consecutive with non-temporal stores
+  const int m = tuning().sweep_lane_pixels;
+  if (m == 1) launch_k_sweep_lp<OutT, VEC, true, false>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+  else if (m == 2) launch_k_sweep_lp<OutT, VEC, false, true>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
+  else launch_k_sweep_lp<OutT, VEC, false, false>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
 }
 
 static size_t sweep_ws_bytes(int B, int C, int h, int w) {

@@ -37,7 +37,7 @@ for rnd in range(3):
             E, P, inl, _ = hp.pose(flow, K)
             assert torch.equal(E, E0) and torch.equal(inl, inl0), "results changed with solve_lanes"
         _lib.tune("solve_lanes", 32)
-    for lp in (0, 1):
+    for lp in (0, 1, 2):
         _lib.tune("sweep_lane_pixels", lp)
         for ipb in (2, 4, 8):
             _lib.tune("sweep_items_per_block", ipb)
