@@ -93,6 +93,18 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
 // Sturm iterations): only `lanes` lanes of each wave carry a hypothesis, so a
 // pair's 4096 hypotheses occupy 4096 / lanes waves and every CU has several
 // independent instruction streams to hide the scratch latency.
+#ifdef SFM_SOLVE_STATS
+// experiment builds only: summed cycles per solve phase (sample+load, basis,
+// equations, reduce, determinant, roots, E+cheirality) over all hypotheses
+__device__ unsigned long long g_solve_stats[8];
+extern "C" int sfm_experiment_solve_stats(unsigned long long* out8) {
+  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_solve_stats), 64) == hipSuccess ? 0 : 2;
+}
+#define SOLVE_T(i) do { const unsigned long long t_ = clock64(); atomicAdd(&g_solve_stats[i], t_ - t0_); t0_ = t_; } while (0)
+#else
+#define SOLVE_T(i) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, int64_t n_stride,
                                               PairParams pp, int H, uint64_t seed, int cheir, int lanes,
                                               int32_t* __restrict__ out_nroots, int32_t* __restrict__ out_ncand,
@@ -102,6 +114,9 @@ __global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, in
   const int h = blockIdx.x * lanes + threadIdx.x;
   if (h >= H) return;
   const int64_t n = pp.n[b];
+#ifdef SFM_SOLVE_STATS
+  unsigned long long t0_ = clock64();
+#endif
   int64_t idx[5];
   sample5(seed, (uint32_t)h, n, idx);
   const double* P = pts + (size_t)b * n_stride * 4;
@@ -111,17 +126,23 @@ __global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, in
     const double4 v = *reinterpret_cast<const double4*>(P + idx[d] * 4);
     q[d][0] = v.x; q[d][1] = v.y; qp[d][0] = v.z; qp[d][1] = v.w;
   }
+  SOLVE_T(0);
   Lin Eb[9];
   essential_basis(q, qp, Eb);
+  SOLVE_T(1);
   Eqs A;
   build_equations(Eb, A);
+  SOLVE_T(2);
   reduce_equations(A);
+  SOLVE_T(3);
   double poly[11];
   determinant_poly(A, poly);
+  SOLVE_T(4);
   double roots[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) roots[i] = 0.0;
   const int nr = real_roots(poly, roots);
+  SOLVE_T(5);
   const int nv = nr > 0 ? (nr < 10 ? nr : 10) : 0;
   const size_t hb = (size_t)b * H + h;
   double* Eo = hypE + hb * kMaxSlots * 9;
@@ -151,6 +172,7 @@ __global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, in
       for (int e = 0; e < 9; ++e) Eo[e] = E[e];
     }
   }
+  SOLVE_T(6);
   out_nroots[hb] = nr;
   out_ncand[hb] = nc;
 }

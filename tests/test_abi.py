@@ -77,3 +77,38 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 src = open(os.path.join(dp, f)).read()
                 assert "oracle" not in re.sub(r"#.*|//.*", "", src).lower().replace("oracle/", ""), f
+
+
+def test_new_entry_points_validate_arguments():
+    """Argument checks of the later entry points fail loudly without touching
+    the device (no GPU here)."""
+    from sfm_amd import _lib
+    lib = _lib.load()
+    v = ctypes.c_void_p(8)
+    n = (ctypes.c_int64 * 2)(5, 7)
+    # keypoints: bad mode, SIFT_POSE without target keypoints, counts beyond the stride
+    assert lib.sfm_keypoints_to_points(v, 2, 10, 10, 10, 10, v, None, 8, n, 3, v, v, 8, None) == 1
+    assert lib.sfm_keypoints_to_points(None, 2, 10, 10, 10, 10, v, None, 8, n, 2, v, v, 8, None) == 1
+    assert b"target" in lib.sfm_last_error()
+    assert lib.sfm_keypoints_to_points(v, 2, 10, 10, 10, 10, v, None, 6, n, 0, v, v, 8, None) == 1
+    # correlation: workspace query and missing workspace
+    assert lib.sfm_correlation_workspace_bytes(2, 32, 10, 20) > 0
+    assert lib.sfm_correlation_workspace_bytes(0, 32, 10, 20) == 0
+    rc = lib.sfm_plane_sweep_correlation(v, v, 1, 4, 8, 8, v, v, v, 4, 1.0, 0, v, None, 0, None)
+    assert rc == 3 and b"workspace" in lib.sfm_last_error()
+    assert lib.sfm_plane_sweep_correlation(v, v, 1, 4, 8, 8, v, v, v, 4, 1.0, 2, v, v, 1 << 20, None) == 1
+    # depth head: PREDICT_BY_DEPTH needs a positive step; bad mode
+    assert lib.sfm_depth_head(v, 1, 8, 4, 4, 16, 16, 1, 1.0, 0.0, v, None) == 1
+    assert lib.sfm_depth_head(v, 1, 8, 4, 4, 16, 16, 5, 1.0, 1.0, v, None) == 1
+    # GPU IRLS: counts beyond the stride, negative reps, too-small workspace
+    assert lib.sfm_essential_optimise_workspace_bytes(2, 1000) > 0
+    assert lib.sfm_essential_optimise_batched(v, 6, n, 2, v, 1e-3, 0.0, 10, v, v, 1 << 20, None) == 1
+    assert lib.sfm_essential_optimise_batched(v, 8, n, 2, v, 1e-3, 0.0, -1, v, v, 1 << 20, None) == 1
+    rc = lib.sfm_essential_optimise_batched(v, 8, n, 2, v, 1e-3, 0.0, 10, v, v, 16, None)
+    assert rc == 3 and b"workspace" in lib.sfm_last_error()
+    # plane sweep ex: bad depth mode, non-positive min depth
+    assert lib.sfm_plane_sweep_ex(v, v, 1, 4, 8, 8, v, v, v, 4, 1.0, 2, 0, v, v, 1 << 20, None) == 1
+    assert lib.sfm_plane_sweep_ex(v, v, 1, 4, 8, 8, v, v, v, 4, 0.0, 0, 0, v, v, 1 << 20, None) == 1
+    # tuning knobs: unknown key / out of range
+    assert lib.sfm_tune_set(b"no_such_knob", 1) == 1
+    assert lib.sfm_tune_set(b"sweep_items_per_block", 3) == 1
