@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--threshold", type=float, default=1e-4)
     ap.add_argument("--cost-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fused", action="store_true",
+                    help="RANSAC reads the flow directly (sfm_ransac5_flow) instead of materialised correspondences")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
 
@@ -116,7 +118,7 @@ def main():
     flow, K, pose_gt, _ = synth.kitti_pair_batch(B, seed=1000 + rank, hw=hw, device=dev)
     ref_fea, tgt_fea = synth.features(B, C, fhw[0], fhw[1], seed=rank, device=dev)
     hp = TwoViewHotPath(B, hw, fhw, C, args.nlabel, args.iters, args.threshold, 1.0, rescale_depth=True,
-                        norm_target=0.6, cost_dtype=cost_dtype, device=dev)
+                        norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused)
 
     for _ in range(args.warmup):
         hp.step(flow, K, ref_fea, tgt_fea)
@@ -139,6 +141,8 @@ def main():
         ms, n = _lib.profile_read(name)
         kt[name] = ms / max(n, 1)
     cands = ransac.candidate_counts(hp.ws, B, args.iters)
+    if hp.fused:
+        kt.pop("flow_to_points", None)
     evals = sum(cands) * hp.n                       # candidate E x correspondences per launch
     score_ms = kt["ransac_score"]
     score_tflops = evals * FLOP_PER_EVAL / (score_ms * 1e-3) / 1e12

@@ -87,6 +87,52 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
 }
 
 // ---------------------------------------------------------------------------
+// Correspondence sources.  The kernels read point k of pair b through one of
+//   PackedSrc  packed (x, y, x', y') float64 rows (sfm_ransac5_packed)
+//   FlowSrc    the dense flow itself: pixel (u, v) of the margin crop, q =
+//              K^-1 (u, v, 1), qp = K^-1 (u + fu, v + fv, 1) in float32 rows
+//              (k0*x + k1*y) + k2, widened (SFMnet.py:179-263, flow2coord
+//              298-318) -- the fused path of SURVEY §8(f) row 2: no staging
+//              buffer, 8 bytes of flow per point instead of 32.
+// Both yield bit-identical values (k_flow_points uses FlowSrc).
+// ---------------------------------------------------------------------------
+struct PackedSrc {
+  const double* pts;
+  int64_t n_stride;
+  __device__ __forceinline__ double4 load(int b, int64_t k) const {
+    return *reinterpret_cast<const double4*>(pts + ((size_t)b * n_stride + k) * 4);
+  }
+  PackedSrc shifted(int b0) const { return PackedSrc{pts + (size_t)b0 * n_stride * 4, n_stride}; }
+};
+
+struct FlowSrc {
+  const float* flow;   // [B][2][H][W]
+  const float* Kinv;   // [B][3][3]
+  int H, W, wn, margin;
+  double inv_wn;       // 1 / wn: k / wn by one multiply and one exact correction (k < 2^31)
+  __device__ __forceinline__ double4 load(int b, int64_t k64) const {
+    const int k = (int)k64;
+    int row = (int)((double)k * inv_wn);
+    int col = k - row * wn;
+    if (col < 0) { --row; col += wn; } else if (col >= wn) { ++row; col -= wn; }
+    const int v = row + margin, u = col + margin;
+    const float* Ki = Kinv + b * 9;
+    const float* F = flow + (size_t)b * 2 * H * W;
+    const float fu = F[(size_t)v * W + u], fv = F[(size_t)H * W + (size_t)v * W + u];
+    const float u1 = (float)u, v1 = (float)v;
+    const float u2 = u1 + fu, v2 = v1 + fv;
+    const float x1 = (Ki[0] * u1 + Ki[1] * v1) + Ki[2];
+    const float y1 = (Ki[3] * u1 + Ki[4] * v1) + Ki[5];
+    const float x2 = (Ki[0] * u2 + Ki[1] * v2) + Ki[2];
+    const float y2 = (Ki[3] * u2 + Ki[4] * v2) + Ki[5];
+    return make_double4(x1, y1, x2, y2);
+  }
+  FlowSrc shifted(int b0) const {
+    return FlowSrc{flow + (size_t)b0 * 2 * H * W, Kinv + (size_t)b0 * 9, H, W, wn, margin, inv_wn};
+  }
+};
+
+// ---------------------------------------------------------------------------
 // Phase 1: one lane per hypothesis
 // ---------------------------------------------------------------------------
 // The solve is latency-bound (scratch-resident polynomial state, data-dependent
@@ -105,8 +151,8 @@ extern "C" int sfm_experiment_solve_stats(unsigned long long* out8) {
 #define SOLVE_T(i) do {} while (0)
 #endif
 
-__global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, int64_t n_stride,
-                                              PairParams pp, int H, uint64_t seed, int cheir, int lanes,
+template <class Src>
+__global__ __launch_bounds__(64) void k_solve(const Src src, PairParams pp, int H, uint64_t seed, int cheir, int lanes,
                                               int32_t* __restrict__ out_nroots, int32_t* __restrict__ out_ncand,
                                               double* __restrict__ hypE, double* __restrict__ hypP) {
   const int b = blockIdx.y;
@@ -119,11 +165,10 @@ __global__ __launch_bounds__(64) void k_solve(const double* __restrict__ pts, in
 #endif
   int64_t idx[5];
   sample5(seed, (uint32_t)h, n, idx);
-  const double* P = pts + (size_t)b * n_stride * 4;
   double q[5][2], qp[5][2];
 #pragma unroll
   for (int d = 0; d < 5; ++d) {
-    const double4 v = *reinterpret_cast<const double4*>(P + idx[d] * 4);
+    const double4 v = src.load(b, idx[d]);
     q[d][0] = v.x; q[d][1] = v.y; qp[d][0] = v.z; qp[d][1] = v.w;
   }
   SOLVE_T(0);
@@ -423,9 +468,8 @@ __device__ __forceinline__ void score_chunk(const double* __restrict__ CE, int n
   }
 }
 
-template <bool FAST>
-__global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restrict__ pts, int64_t n_stride,
-                                                         PairParams pp, int batch, int cmax,
+template <bool FAST, class Src>
+__global__ __launch_bounds__(kScoreThreads) void k_score(const Src src, PairParams pp, int batch, int cmax,
                                                          const int32_t* __restrict__ cand_total,
                                                          const double* __restrict__ candE,
                                                          int32_t* __restrict__ cntT, int32_t* __restrict__ cntR,
@@ -460,7 +504,6 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restric
     const int M = max(T, R);
     const int p0 = split * kPtsPerItem;
     const int p1 = min(M, p0 + kPtsPerItem);
-    const double* P = pts + (size_t)b * n_stride * 4;
     const double* CE = candE + ((size_t)b * cmax + c0) * kCandStride;
     for (int cb = p0; cb < p1; cb += kChunk) {
       double x[kPPL], y[kPPL], xp[kPPL], yp[kPPL], mm2[kPPL];
@@ -470,7 +513,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const double* __restric
       for (int k = 0; k < kPPL; ++k) {
         const int p = cb + k * kScoreThreads + tid;
         const bool ok = p < p1;
-        const double4 v = *reinterpret_cast<const double4*>(P + (size_t)(ok ? p : p0) * 4);
+        const double4 v = src.load(b, ok ? p : p0);
         x[k] = v.x; y[k] = v.y; xp[k] = v.z; yp[k] = v.w;
         mm2[k] = point_scale(v.x, v.y, v.z, v.w);
         unit = unit && (mm2[k] == 1.0);
@@ -527,9 +570,10 @@ extern "C" int sfm_experiment_score_stats(unsigned long long* out3) {
 #endif
 
 // float64 decision of one point (reloaded); guard per point (any scale)
-__device__ __forceinline__ bool inlier_f64(const double* __restrict__ Ec, const double* __restrict__ P, int p,
+template <class Src>
+__device__ __forceinline__ bool inlier_f64(const double* __restrict__ Ec, const Src& src, int b, int p,
                                            const ScoreConsts& kc) {
-  const double4 v = *reinterpret_cast<const double4*>(P + (size_t)p * 4);
+  const double4 v = src.load(b, p);
   double E[9];
 #pragma unroll
   for (int e = 0; e < 9; ++e) E[e] = Ec[e];
@@ -544,8 +588,8 @@ __device__ __forceinline__ bool inlier_f64(const double* __restrict__ Ec, const 
 // point.  Undecided points are re-tested in float64 after the unrolled loop.
 constexpr int kQueue = 1024;   // undecided (candidate, point) entries per wave (LDS)
 
-template <bool SAME, bool MASKED>
-__device__ __forceinline__ void score32_chunk(const double* __restrict__ CE, int nc, const double* __restrict__ P,
+template <bool SAME, bool MASKED, class Src>
+__device__ __forceinline__ void score32_chunk(const double* __restrict__ CE, int nc, const Src& src, int b,
                                               int cb, int tid, int p1, int T, int R, const float (&x)[kPPL],
                                               const float (&y)[kPPL], const float (&xp)[kPPL],
                                               const float (&yp)[kPPL], const uint64_t (&mT)[kPPL],
@@ -638,7 +682,7 @@ __device__ __forceinline__ void score32_chunk(const double* __restrict__ CE, int
           if (!und[k]) continue;
           const int p = cb + k * kScoreThreads + tid;
           bool in = false;
-          if ((und[k] >> lane) & 1ull) in = inlier_f64(Ec, P, p, kc);
+          if ((und[k] >> lane) & 1ull) in = inlier_f64(Ec, src, b, p, kc);
           const uint64_t m = __ballot(in);
           if (MASKED) {
             sT += __popcll(m & mT[k]);
@@ -661,15 +705,15 @@ __device__ __forceinline__ void score32_chunk(const double* __restrict__ CE, int
   for (int i = lane; i < qn; i += 64) {
     const uint32_t e = q[i];
     const int c = (int)(e >> 24), p = (int)(e & 0xffffffu);
-    if (inlier_f64(CE + (size_t)c * kCandStride, P, p, kc)) {
+    if (inlier_f64(CE + (size_t)c * kCandStride, src, b, p, kc)) {
       if (p < T) atomicAdd(&cnt[c][0], 1);
       if (p < R) atomicAdd(&cnt[c][1], 1);
     }
   }
 }
 
-__global__ __launch_bounds__(kScoreThreads) void k_score32(const double* __restrict__ pts, int64_t n_stride,
-                                                           PairParams pp, int batch, int cmax,
+template <class Src>
+__global__ __launch_bounds__(kScoreThreads) void k_score32(const Src src, PairParams pp, int batch, int cmax,
                                                            const int32_t* __restrict__ cand_total,
                                                            const double* __restrict__ candE,
                                                            int32_t* __restrict__ cntT, int32_t* __restrict__ cntR,
@@ -707,7 +751,6 @@ __global__ __launch_bounds__(kScoreThreads) void k_score32(const double* __restr
     const int M = max(T, R);
     const int p0 = split * kPtsPerItem;
     const int p1 = min(M, p0 + kPtsPerItem);
-    const double* P = pts + (size_t)b * n_stride * 4;
     {
       // stage the tile's candidate records (nc x 128 B) in LDS
       const double2* src = reinterpret_cast<const double2*>(candE + ((size_t)b * cmax + c0) * kCandStride);
@@ -723,7 +766,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score32(const double* __restr
 #pragma unroll
       for (int k = 0; k < kPPL; ++k) {
         const int p = cb + k * kScoreThreads + tid;
-        const double4 v = *reinterpret_cast<const double4*>(P + (size_t)min(p, p1 - 1) * 4);
+        const double4 v = src.load(b, min(p, p1 - 1));
         M = fmax(M, fmax(fmax(fabs(v.x), fabs(v.y)), fmax(fabs(v.z), fabs(v.w))));
         x[k] = (float)v.x; y[k] = (float)v.y; xp[k] = (float)v.z; yp[k] = (float)v.w;
         mT[k] = __ballot(p < p1 && p < T);
@@ -736,13 +779,13 @@ __global__ __launch_bounds__(kScoreThreads) void k_score32(const double* __restr
       const float M2 = Mf * Mf;
       const bool full = cb + kChunk <= min(T, R);                 // no prefix masking needed
       if (full) {
-        score32_chunk<true, false>(CE, nc, P, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
+        score32_chunk<true, false>(CE, nc, src, b, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
                                    s_cnt[wv], s_queue[wv]);
       } else if (T == R) {
-        score32_chunk<true, true>(CE, nc, P, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
+        score32_chunk<true, true>(CE, nc, src, b, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
                                   s_cnt[wv], s_queue[wv]);
       } else {
-        score32_chunk<false, true>(CE, nc, P, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
+        score32_chunk<false, true>(CE, nc, src, b, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
                                    s_cnt[wv], s_queue[wv]);
       }
     }
@@ -850,25 +893,13 @@ __global__ void k_pack(const double* __restrict__ q, const double* __restrict__ 
   reinterpret_cast<double4*>(out)[k] = make_double4(a.x, a.y, c.x, c.y);
 }
 
-// flow2coord + margin crop + K^-1 (models/SFMnet.py:179-263, 298-318)
-__global__ void k_flow_points(const float* __restrict__ flow, int H, int W, int h_side, int w_side, int margin,
-                              const float* __restrict__ Kinv, double* __restrict__ out) {
+// flow2coord + margin crop + K^-1 (models/SFMnet.py:179-263, 298-318): the
+// FlowSrc values, materialised
+__global__ void k_flow_points(const FlowSrc src, int64_t N, double* __restrict__ out) {
   const int b = blockIdx.y;
-  const int wn = w_side - 2 * margin, hn = h_side - 2 * margin;
-  const int64_t N = (int64_t)wn * hn;
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= N) return;
-  const int v = (int)(k / wn) + margin, u = (int)(k % wn) + margin;
-  const float* Ki = Kinv + b * 9;
-  const float* F = flow + (size_t)b * 2 * H * W;
-  const float fu = F[(size_t)v * W + u], fv = F[(size_t)H * W + (size_t)v * W + u];
-  const float u1 = (float)u, v1 = (float)v;
-  const float u2 = u1 + fu, v2 = v1 + fv;
-  const float x1 = (Ki[0] * u1 + Ki[1] * v1) + Ki[2];
-  const float y1 = (Ki[3] * u1 + Ki[4] * v1) + Ki[5];
-  const float x2 = (Ki[0] * u2 + Ki[1] * v2) + Ki[2];
-  const float y2 = (Ki[3] * u2 + Ki[4] * v2) + Ki[5];
-  reinterpret_cast<double4*>(out)[(size_t)b * N + k] = make_double4(x1, y1, x2, y2);
+  reinterpret_cast<double4*>(out)[(size_t)b * N + k] = src.load(b, k);
 }
 
 // Sparse correspondences of SFMnet.pose_by_ransac (models/SFMnet.py:218-258):
@@ -949,7 +980,8 @@ __global__ void k_keypoint_points(const float* __restrict__ flow, int H, int W, 
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
-static int run_chunk(const double* pts, int64_t n_stride, const int64_t* n, int bc, int num_test,
+template <class Src>
+static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
                      const Workspace& w, double* E_out, double* P_out, int32_t* inliers_out,
                      int32_t* winner_out, int32_t* score_out, hipStream_t s) {
@@ -966,7 +998,7 @@ static int run_chunk(const double* pts, int64_t n_stride, const int64_t* n, int 
   {
     ProfScope ps("ransac_solve", s);
     const int lanes = tuning().solve_lanes;
-    hipLaunchKernelGGL(k_solve, dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, pts, n_stride, pp, H, seed, cheir,
+    hipLaunchKernelGGL(k_solve<Src>, dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H, seed, cheir,
                        lanes,
                        w.nroots, w.ncand, w.hypE, w.hypP);
   }
@@ -996,13 +1028,13 @@ static int run_chunk(const double* pts, int64_t n_stride, const int64_t* n, int 
   {
     ProfScope ps("ransac_score", s);
     if (fast32)
-      hipLaunchKernelGGL(k_score32, dim3(grid), dim3(kScoreThreads), 0, s, pts, n_stride, pp, bc, cmax,
+      hipLaunchKernelGGL(k_score32<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.cntT, w.cntR, kc);
     else if (fast)
-      hipLaunchKernelGGL(k_score<true>, dim3(grid), dim3(kScoreThreads), 0, s, pts, n_stride, pp, bc, cmax,
+      hipLaunchKernelGGL((k_score<true, Src>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.cntT, w.cntR, kc);
     else
-      hipLaunchKernelGGL(k_score<false>, dim3(grid), dim3(kScoreThreads), 0, s, pts, n_stride, pp, bc, cmax,
+      hipLaunchKernelGGL((k_score<false, Src>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.cntT, w.cntR, kc);
   }
   SFM_LAUNCHED();
@@ -1023,6 +1055,30 @@ static int check_common(int iters, double thr, int batch) {
   return SFM_OK;
 }
 
+template <class Src>
+static int run_src(const Src& src, const int64_t* n, int batch, int num_test, int num_ransac_test, int iters,
+                   double thr, uint64_t seed, int cheir, void* ws, size_t ws_bytes, double* E_out, double* P_out,
+                   int32_t* inliers_out, int32_t* winner_out, int32_t* score_out, hipStream_t s) {
+  const int bc = std::min(batch, SFM_MAX_BATCH);
+  const size_t need = layout(nullptr, bc, 0, iters, nullptr);
+  if (!ws || ws_bytes < need) {
+    set_error("workspace too small: need " + std::to_string(need) + " bytes");
+    return SFM_ERR_WORKSPACE;
+  }
+  Workspace w;
+  layout((char*)ws, bc, 0, iters, &w);
+  const int H = kChains * iters;
+  for (int b0 = 0; b0 < batch; b0 += bc) {
+    const int nb = std::min(bc, batch - b0);
+    if (int rc = run_chunk(src.shifted(b0), n + b0, nb, num_test, num_ransac_test, iters, thr, seed, cheir, w,
+                           E_out + (size_t)b0 * 9, P_out ? P_out + (size_t)b0 * 12 : nullptr, inliers_out + b0,
+                           winner_out ? winner_out + b0 : nullptr,
+                           score_out ? score_out + (size_t)b0 * H : nullptr, s))
+      return rc;
+  }
+  return SFM_OK;
+}
+
 static int run_packed(const double* pts, int64_t n_stride, const int64_t* n, int batch, int num_test,
                       int num_ransac_test, int iters, double thr, uint64_t seed, int cheir, void* ws,
                       size_t ws_bytes, double* E_out, double* P_out, int32_t* inliers_out, int32_t* winner_out,
@@ -1036,24 +1092,8 @@ static int run_packed(const double* pts, int64_t n_stride, const int64_t* n, int
     SFM_REQUIRE(num_test <= n[b] && num_ransac_test <= n[b],
                 "num_test_points / num_ransac_test_points must not exceed the number of points");
   }
-  const int bc = std::min(batch, SFM_MAX_BATCH);
-  const size_t need = layout(nullptr, bc, 0, iters, nullptr);
-  if (!ws || ws_bytes < need) {
-    set_error("workspace too small: need " + std::to_string(need) + " bytes");
-    return SFM_ERR_WORKSPACE;
-  }
-  Workspace w;
-  layout((char*)ws, bc, 0, iters, &w);
-  const int H = kChains * iters;
-  for (int b0 = 0; b0 < batch; b0 += bc) {
-    const int nb = std::min(bc, batch - b0);
-    if (int rc = run_chunk(pts + (size_t)b0 * n_stride * 4, n_stride, n + b0, nb, num_test, num_ransac_test,
-                           iters, thr, seed, cheir, w, E_out + (size_t)b0 * 9, P_out ? P_out + (size_t)b0 * 12 : nullptr,
-                           inliers_out + b0, winner_out ? winner_out + b0 : nullptr,
-                           score_out ? score_out + (size_t)b0 * H : nullptr, s))
-      return rc;
-  }
-  return SFM_OK;
+  return run_src(PackedSrc{pts, n_stride}, n, batch, num_test, num_ransac_test, iters, thr, seed, cheir, ws,
+                 ws_bytes, E_out, P_out, inliers_out, winner_out, score_out, s);
 }
 
 }  // namespace sfm
@@ -1094,6 +1134,26 @@ int sfm_ransac5_packed(const double* pts, int64_t n_stride, const int64_t* n, in
                        int32_t* inliers_out, int32_t* winner_out, int32_t* hyp_score_out, void* stream) {
   return run_packed(pts, n_stride, n, batch, num_test, num_ransac_test, iters, thr, seed, cheirality, workspace,
                     workspace_bytes, E_out, P_out, inliers_out, winner_out, hyp_score_out, (hipStream_t)stream);
+}
+
+int sfm_ransac5_flow(const float* flow, int batch, int H, int W, int h_side, int w_side, int margin,
+                     const float* Kinv, int num_test, int num_ransac_test, int iters, double thr, uint64_t seed,
+                     int cheirality, void* workspace, size_t workspace_bytes, double* E_out, double* P_out,
+                     int32_t* inliers_out, int32_t* winner_out, int32_t* hyp_score_out, void* stream) {
+  if (int rc = check_common(iters, thr, batch)) return rc;
+  SFM_REQUIRE(flow && Kinv && E_out && inliers_out, "null pointer argument");
+  SFM_REQUIRE(cheirality == 0 || P_out, "P_out required when cheirality is on");
+  SFM_REQUIRE(H >= 1 && W >= 1 && h_side >= 1 && h_side <= H && w_side >= 1 && w_side <= W,
+              "h_side/w_side out of range");
+  SFM_REQUIRE(margin >= 0 && 2 * margin < h_side && 2 * margin < w_side, "margin leaves no pixels");
+  const int64_t N = (int64_t)(h_side - 2 * margin) * (w_side - 2 * margin);
+  SFM_REQUIRE(N >= 5 && N <= (int64_t)INT32_MAX, "point count out of range");
+  SFM_REQUIRE(num_test <= N && num_ransac_test <= N,
+              "num_test_points / num_ransac_test_points must not exceed the number of points");
+  std::vector<int64_t> n((size_t)batch, N);
+  const FlowSrc src{flow, Kinv, H, W, w_side - 2 * margin, margin, 1.0 / (double)(w_side - 2 * margin)};
+  return run_src(src, n.data(), batch, num_test, num_ransac_test, iters, thr, seed, cheirality, workspace,
+                 workspace_bytes, E_out, P_out, inliers_out, winner_out, hyp_score_out, (hipStream_t)stream);
 }
 
 int sfm_ransac5_inlier_mask(const double* pts, int64_t n_stride, const int64_t* n, int batch, const double* E,
@@ -1147,8 +1207,9 @@ int sfm_flow_to_points(const float* flow, int batch, int H, int W, int h_side, i
   for (int b0 = 0; b0 < batch; b0 += 65535) {
     const int nb = std::min(65535, batch - b0);
     ProfScope ps("flow_to_points", s);
-    hipLaunchKernelGGL(k_flow_points, dim3((unsigned)((N + 255) / 256), nb), dim3(256), 0, s,
-                       flow + (size_t)b0 * 2 * H * W, H, W, h_side, w_side, margin, Kinv + (size_t)b0 * 9,
+    const FlowSrc src{flow + (size_t)b0 * 2 * H * W, Kinv + (size_t)b0 * 9, H, W, w_side - 2 * margin, margin,
+                      1.0 / (double)(w_side - 2 * margin)};
+    hipLaunchKernelGGL(k_flow_points, dim3((unsigned)((N + 255) / 256), nb), dim3(256), 0, s, src, N,
                        pts_out + (size_t)b0 * N * 4);
   }
   SFM_LAUNCHED();

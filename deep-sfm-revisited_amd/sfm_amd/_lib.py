@@ -47,6 +47,10 @@ _SIGS = [
     ("sfm_plane_sweep_warped", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
       ctypes.c_float, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),
+    ("sfm_ransac5_flow", ctypes.c_int,
+     [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp,
+      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.c_int, _c_dp,
+      ctypes.c_size_t, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp]),
     ("sfm_keypoints_to_points", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, ctypes.c_int64,
       _c_dp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_int64, _c_dp]),

@@ -6,6 +6,7 @@ GPU, exactly the work SFMnet.forward does between the flow estimator and the
 branch of pose_by_ransac 176-274, and PSNet.py:130-158):
 
   1. correspondences from the flow (margin 10, K^-1)      sfm_flow_to_points
+     (fused=True: read on the fly by the RANSAC kernels,   sfm_ransac5_flow)
   2. RANSAC five-point E / P per pair (H = 512 x iters)    sfm_ransac5_packed
   3. P -> pose, optional RESCALE_DEPTH translation scaling
   4. cost volume [B, 2C, L, h, w] at quarter resolution    sfm_plane_sweep
@@ -21,7 +22,7 @@ from . import ransac, sweep
 class TwoViewHotPath:
     def __init__(self, batch, image_hw, feat_hw, channels=32, nlabel=128, iters=8, threshold=1e-4,
                  min_depth=1.0, rescale_depth=False, norm_target=0.6, cost_dtype=torch.float32, margin=10,
-                 device="cuda", seed=ransac.DEFAULT_SEED):
+                 device="cuda", seed=ransac.DEFAULT_SEED, fused=False):
         self.batch = int(batch)
         self.H, self.W = image_hw
         self.h, self.w = feat_hw
@@ -35,8 +36,10 @@ class TwoViewHotPath:
         self.seed = int(seed)
         self.device = torch.device(device)
         self.n = (self.H - 2 * margin) * (self.W - 2 * margin)
+        self.fused = bool(fused)
         B = self.batch
-        self.pts = torch.empty(B, self.n, 4, dtype=torch.float64, device=self.device)
+        # fused: RANSAC reads the flow directly (no correspondence buffer)
+        self.pts = None if self.fused else torch.empty(B, self.n, 4, dtype=torch.float64, device=self.device)
         self.ws = ransac.workspace_for(B, self.iters, self.device)
         self.cost = torch.empty(B, 2 * self.C, self.L, self.h, self.w, dtype=cost_dtype, device=self.device)
         self.cost_dtype = cost_dtype
@@ -44,6 +47,9 @@ class TwoViewHotPath:
 
     def pose(self, flow, K):
         Kinv = torch.inverse(K.float())
+        if self.fused:
+            return ransac.ransac5_flow(flow, Kinv, self.iters, self.thr, self.H, self.W, self.margin, seed=self.seed,
+                                       workspace=self.ws)
         ransac.flow_to_points(flow, Kinv, self.H, self.W, self.margin, out=self.pts)
         E, P, inl, win = ransac.ransac5_batched(self.pts, None, None, None, self.iters, self.thr, self.seed,
                                                 True, workspace=self.ws)

@@ -231,3 +231,36 @@ def optimise_batched(pts, E_init, delta=0.001, alpha=0.0, max_reps=200, n=None, 
                                               workspace.numel(), _lib.stream_ptr(pts.device))
         _lib.check(rc, "sfm_essential_optimise_batched")
     return out
+
+
+def ransac5_flow(flow, intrinsic_inv, iters=5, threshold=1e-4, h_side=None, w_side=None, margin=10,
+                 num_test_points=None, num_ransac_test_points=None, seed=DEFAULT_SEED, cheirality=True,
+                 return_scores=False, workspace=None):
+    """Fused dense path (SFMnet.py:179-274 without the correspondence buffer):
+    RANSAC straight from flow [B,2,H,W] float32 and K^-1 [B,3,3] (CUDA).
+    Bit-identical to ransac5_batched(flow_to_points(flow, K^-1), ...)."""
+    if not flow.is_cuda:
+        raise RuntimeError("flow must be a CUDA tensor")
+    flow = flow.contiguous().float()
+    Ki = intrinsic_inv.contiguous().float()
+    B, _, H, W = flow.shape
+    h = H if h_side is None else int(h_side)
+    w = W if w_side is None else int(w_side)
+    dev = flow.device
+    Hh = hypotheses(iters)
+    with torch.cuda.device(dev):
+        if workspace is None:
+            workspace = _workspace(B, 0, iters, dev)
+        E = torch.empty(B, 3, 3, dtype=torch.float64, device=dev)
+        P = torch.empty(B, 3, 4, dtype=torch.float64, device=dev) if cheirality else None
+        inl = torch.empty(B, dtype=torch.int32, device=dev)
+        win = torch.empty(B, dtype=torch.int32, device=dev)
+        scores = torch.empty(B, Hh, dtype=torch.int32, device=dev) if return_scores else None
+        rc = _lib.load().sfm_ransac5_flow(
+            _lib.ptr(flow), B, H, W, h, w, int(margin), _lib.ptr(Ki), int(num_test_points or 0),
+            int(num_ransac_test_points or 0), int(iters), float(threshold), int(seed), 1 if cheirality else 0,
+            _lib.ptr(workspace), workspace.numel(), _lib.ptr(E), _lib.ptr(P), _lib.ptr(inl), _lib.ptr(win),
+            _lib.ptr(scores), _lib.stream_ptr(dev))
+        _lib.check(rc, "sfm_ransac5_flow")
+    out = (E, P, inl, win)
+    return out + (scores,) if return_scores else out

@@ -99,6 +99,19 @@ int sfm_ransac5_packed(const double* pts, int64_t n_stride, const int64_t* n, in
                        double* E_out, double* P_out, int32_t* inliers_out, int32_t* winner_out,
                        int32_t* hyp_score_out, void* stream);
 
+/* Fused dense path: RANSAC straight from the flow
+ * field, no correspondence buffer.  Point k of each pair is pixel
+ * (u, v) = (m + k % (w_side-2m), m + k / (w_side-2m)) of the crop, with the
+ * values of sfm_flow_to_points (bit-identical results to
+ * sfm_flow_to_points + sfm_ransac5_packed).
+ *   flow [dev] batch x 2 x H x W float32; Kinv [dev] batch x 3 x 3 float32;
+ *   other arguments and outputs as sfm_ransac5_packed. */
+int sfm_ransac5_flow(const float* flow, int batch, int H, int W, int h_side, int w_side, int margin,
+                     const float* Kinv, int num_test, int num_ransac_test, int iters, double thr,
+                     uint64_t seed, int cheirality, void* workspace, size_t workspace_bytes,
+                     double* E_out, double* P_out, int32_t* inliers_out, int32_t* winner_out,
+                     int32_t* hyp_score_out, void* stream);
+
 /* Exact inlier mask of E (reference ComputeError + `<= thr`) for each point.
  *   pts [dev] batch x n_stride x 4; n [host] batch; E [dev] batch x 9;
  *   mask [dev] batch x n_stride uint8 (entries >= n[b] are written 0). */

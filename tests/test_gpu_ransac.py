@@ -179,3 +179,18 @@ def test_fp32_predecision_is_exact(cuda):
     p = pts[0].cpu().numpy()
     r = ORR.ransac5(p[:, :2], p[:, 2:], iters=2, thr=1e-4)
     assert np.array_equal(outs[0][4][0].cpu().numpy(), r["hyp_score"])
+
+
+def test_fused_flow_path_equals_packed(cuda):
+    """sfm_ransac5_flow (correspondences read from the flow on the fly) is
+    bit-identical to flow_to_points + ransac5_batched, crop and margin included."""
+    from sfm_amd import ransac, synth
+    flow, K, _, _ = synth.kitti_pair_batch(3, seed=41, hw=(100, 180))
+    Ki = torch.inverse(K.float()).to(cuda)
+    f = flow.to(cuda)
+    for h_side, w_side, margin in ((None, None, 10), (90, 170, 7)):
+        pts = ransac.flow_to_points(f, Ki, h_side, w_side, margin)
+        a = ransac.ransac5_batched(pts, iters=2, threshold=1e-4, return_scores=True)
+        b = ransac.ransac5_flow(f, Ki, 2, 1e-4, h_side, w_side, margin, return_scores=True)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
