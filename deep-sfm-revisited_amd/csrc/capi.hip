@@ -87,6 +87,7 @@ int sfm_tune_set(const char* key, int value) {
   const std::string k(key);
   sfm::Tuning& t = sfm::tuning();
   if (k == "solve_lanes" && value >= 1 && value <= 64) t.solve_lanes = value;
+  else if (k == "roots_lanes" && value >= 1 && value <= 64) t.roots_lanes = value;
   else if (k == "sweep_lane_pixels" && value >= 0 && value <= 2) t.sweep_lane_pixels = value;
   else if (k == "sweep_items_per_block" && (value == 1 || value == 2 || value == 4 || value == 8))
     t.sweep_items_per_block = value;

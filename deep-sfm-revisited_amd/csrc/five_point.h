@@ -611,6 +611,215 @@ __device__ int real_roots(const double poly[11], double roots[10]) {
   return nr;
 }
 
+// ---------------------------------------------------------------------------
+// Register-resident Sturm root isolation (used by k_roots).  After
+// build_sturm, polynomial i of the sequence has degree ord[i] <= 10 - i, so
+// the whole sequence fits a static, zero-padded layout of 66 doubles
+// (polynomial i at offset i*(23-i)/2, 11-i slots).  Horner over the padded
+// coefficients gives bit-identical values to Horner from ord[i]: the padded
+// steps produce x*0 + 0 = +-0 and the first real step (+-0)*x + c = c
+// exactly.  Every loop below is fully unrolled over static indices, so the
+// coefficients stay in registers instead of scratch (the reference-order
+// mul-then-add evaluation is unchanged).
+// ---------------------------------------------------------------------------
+constexpr int sturm_off(int i) { return i * (23 - i) / 2; }
+constexpr int kSturmRegs = sturm_off(11);   // 66
+
+struct SturmR {
+  double c[kSturmRegs];
+  int ord[11];
+  int np;
+};
+
+template <int I>
+__device__ __forceinline__ double horner_r(const SturmR& S, double x) {
+  constexpr int o = sturm_off(I), d = 10 - I;
+  double f = S.c[o + d];
+#pragma unroll
+  for (int j = d - 1; j >= 0; --j) f = x * f + S.c[o + j];
+  return f;
+}
+
+template <int I>
+__device__ __forceinline__ void sign_step(const SturmR& S, double a, double& lf, int& ch) {
+  if (I <= S.np) {
+    const double f = horner_r<I>(S, a);
+    if (lf == 0.0 || lf * f < 0) ++ch;
+    lf = f;
+  }
+}
+
+// numchanges (sturm.cu:369-385)
+__device__ __forceinline__ int sign_changes_r(const SturmR& S, double a) {
+  int ch = 0;
+  double lf = horner_r<0>(S, a);
+  sign_step<1>(S, a, lf, ch); sign_step<2>(S, a, lf, ch); sign_step<3>(S, a, lf, ch);
+  sign_step<4>(S, a, lf, ch); sign_step<5>(S, a, lf, ch); sign_step<6>(S, a, lf, ch);
+  sign_step<7>(S, a, lf, ch); sign_step<8>(S, a, lf, ch); sign_step<9>(S, a, lf, ch);
+  sign_step<10>(S, a, lf, ch);
+  return ch;
+}
+
+// modrf_pos (sturm.cu:43-207) on the register copy of s[0]
+__device__ int falsi_r(const SturmR& S, double a, double b, double* val, bool inv) {
+  const double* c = S.c;   // s[0] occupies c[0..10]
+  if (inv) { double t = a; a = 1.0 / b; b = 1.0 / t; }
+  double fa, fb;
+  if (inv) {
+    fa = fb = c[0];
+#pragma unroll
+    for (int i = 1; i <= 10; ++i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
+  } else {
+    fa = fb = c[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
+  }
+  if (fa * fb > 0.0) return 0;
+  if (fabs(fa) < kRelErr) { *val = inv ? 1.0 / a : a; return 1; }
+  if (fabs(fb) < kRelErr) { *val = inv ? 1.0 / b : b; return 1; }
+  double lfx = fa;
+  for (int it = 0; it < kMaxIt; ++it) {
+    const double x = (fb * a - fa * b) / (fb - fa);
+    double fx;
+    if (inv) {
+      fx = c[0];
+#pragma unroll
+      for (int i = 1; i <= 10; ++i) fx = x * fx + c[i];
+    } else {
+      fx = c[10];
+#pragma unroll
+      for (int i = 9; i >= 0; --i) fx = x * fx + c[i];
+    }
+    if (fabs(x) > kRelErr && fabs(fx / x) < kRelErr) { *val = inv ? 1.0 / x : x; return 1; }
+    else if (fabs(fx) < kRelErr) { *val = inv ? 1.0 / x : x; return 1; }
+    if ((fa * fx) < 0) { b = x; fb = fx; if ((lfx * fx) > 0) fa /= 2; }
+    else { a = x; fa = fx; if ((lfx * fx) > 0) fb /= 2; }
+    if (fabs(b - a) < fabs(kRelErr * a)) { *val = inv ? 1.0 / a : a; return 1; }
+    lfx = fx;
+  }
+  return 0;
+}
+
+// modrf (sturm.cu:218-275), leading coefficient omitted at +-1 as in the reference
+__device__ int falsi_any_r(const SturmR& S, double a, double b, double* val) {
+  const double* c = S.c;
+  if (a > b) { double t = a; a = b; b = t; }
+  if (b <= 1.0 && a >= -1.0) return falsi_r(S, a, b, val, false);
+  if (a >= 1.0 || b <= -1.0) return falsi_r(S, a, b, val, true);
+  double fp1 = 0.0, fm1 = 0.0, fa = 0.0, fb = 0.0;
+#pragma unroll
+  for (int i = 9; i >= 0; --i) {
+    fp1 = c[i] + fp1;
+    fm1 = c[i] - fm1;
+    fa = a * fa + c[i];
+    fb = b * fb + c[i];
+  }
+  if (a < -1.0 && b > 1.0) {
+    if (fa * fm1 < 0.0) return falsi_r(S, a, -1.0, val, true);
+    if (fb * fp1 < 0.0) return falsi_r(S, 1.0, b, val, true);
+    return falsi_r(S, -1.0, 1.0, val, false);
+  }
+  if (a < -1.0) {
+    if (fa * fm1 < 0.0) return falsi_r(S, a, -1.0, val, true);
+    return falsi_r(S, -1.0, b, val, false);
+  }
+  if (fb * fp1 < 0.0) return falsi_r(S, 1.0, b, val, true);
+  return falsi_r(S, a, 1.0, val, false);
+}
+
+// sbisect<depth> (sturm.cu:450-555) as an explicit depth-first work stack
+__device__ void isolate_r(const SturmR& S, double lo, double hi, int atlo, int athi, double roots[10]) {
+  struct Iv { double lo, hi; int atlo, athi, off, depth; };
+  Iv stk[24];
+  int sp = 0;
+  stk[sp++] = Iv{lo, hi, atlo, athi, 0, 0};
+  while (sp > 0) {
+    const Iv iv = stk[--sp];
+    if (iv.depth >= kMaxDepth) continue;
+    double mn = iv.lo, mx = iv.hi, mid = 0.0;
+    if (iv.atlo - iv.athi == 1) {
+      double v;
+      if (falsi_any_r(S, mn, mx, &v)) {
+        if (iv.off >= 0 && iv.off < 10) roots[iv.off] = v;
+        continue;
+      }
+      for (int it = 0; it < kMaxIt; ++it) {
+        mid = (double)((mn + mx) / 2);
+        const int atmid = sign_changes_r(S, mid);
+        if (fabs(mid) > kRelErr) {
+          if (fabs((mx - mn) / mid) < kRelErr) break;
+        } else if (fabs(mx - mn) < kRelErr) break;
+        if ((iv.atlo - atmid) == 0) mn = mid; else mx = mid;
+      }
+      if (iv.off >= 0 && iv.off < 10) roots[iv.off] = mid;
+      continue;
+    }
+    int it;
+    for (it = 0; it < kMaxIt; ++it) {
+      mid = (double)((mn + mx) / 2);
+      const int atmid = sign_changes_r(S, mid);
+      const int n1 = iv.atlo - atmid, n2 = atmid - iv.athi;
+      if (n1 != 0 && n2 != 0) {
+        if (sp + 2 <= 24) {
+          stk[sp++] = Iv{mid, mx, atmid, iv.athi, iv.off + n1, iv.depth + 1};
+          stk[sp++] = Iv{mn, mid, iv.atlo, atmid, iv.off, iv.depth + 1};
+        }
+        break;
+      }
+      if (n1 == 0) mn = mid; else mx = mid;
+    }
+    if (it == kMaxIt)
+      for (int r = iv.athi; r < iv.atlo; ++r) {
+        const int slot = iv.off + r - iv.athi;
+        if (slot >= 0 && slot < 10) roots[slot] = mid;
+      }
+  }
+}
+
+// find_real_roots_sturm (sturm.cu:557-676) with the iterative part on the
+// register-resident sequence; identical results to real_roots.
+__device__ int real_roots_r(const double poly[11], double roots[10]) {
+  SturmR R;
+  {
+    Sturm S;
+    for (int i = 0; i < 11; ++i) { S.ord[i] = 0; for (int j = 0; j < 11; ++j) S.c[i][j] = 0.0; }
+    const double norm = 1.0 / poly[10];
+    for (int i = 0; i <= 10; ++i) S.c[0][i] = poly[i] * norm;
+    const double v0 = fabs(S.c[0][0]);
+    double fac = 1.0;
+    if (v0 > 10.0) {
+      fac = cr_pow(v0, -1.0 / 10);
+      double m = fac;
+      for (int i = 9; i >= 0; --i) { S.c[0][i] *= m; m = m * fac; }
+    }
+    const int np = build_sturm(S);
+    int atmin, atmax;
+    int nr = count_real_roots(S, np, &atmin, &atmax);
+    if (nr == 0) return 0;
+    // register copy, zero above each polynomial's degree
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) {
+      R.ord[i] = S.ord[i];
+#pragma unroll
+      for (int j = 0; j <= 10 - i; ++j) R.c[sturm_off(i) + j] = (i <= np && j <= S.ord[i]) ? S.c[i][j] : 0.0;
+    }
+    R.np = np;
+    double mn = -1.0;
+    int nch = sign_changes_r(R, mn);
+    for (int i = 0; nch != atmin && i != kMaxPow; ++i) { mn *= 10.0; nch = sign_changes_r(R, mn); }
+    if (nch != atmin) atmin = nch;
+    double mx = 1.0;
+    nch = sign_changes_r(R, mx);
+    for (int i = 0; nch != atmax && i != kMaxPow; ++i) { mx *= 10.0; nch = sign_changes_r(R, mx); }
+    if (nch != atmax) atmax = nch;
+    nr = atmin - atmax;
+    if (nr <= 0) return nr;
+    isolate_r(R, mn, mx, atmin, atmax, roots);
+    for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
+    return nr;
+  }
+}
+
 // null_space_solve_3x3_half_pivot (essential_matrix_5pt.cu:476-507)
 __device__ __forceinline__ void null3(double M[3][3], double& x, double& y) {
   int p1;

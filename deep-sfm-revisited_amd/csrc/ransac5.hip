@@ -33,6 +33,9 @@ namespace sfm {
 constexpr int kChains = SFM_RANSAC_CHAINS;
 constexpr int kMaxSlots = 10;
 constexpr int kCandStride = 18;   // per candidate: E f64[9], Kg, then float[14] (E f32[9], A1, B1, A2, B2, ok32)
+// solve state fields: E basis (36), the 3x3 blocks of the reduced equations
+// that compute_E_matrix reads (39), the five samples (20), det poly (11), roots (10)
+constexpr int kStEb = 0, kStA = 36, kStQ = 75, kStPoly = 95, kStRoots = 106, kStateFields = 116;
 constexpr int kKC = 32;           // candidates per score tile
 constexpr int kPPL = 8;           // points per lane per chunk
 constexpr int kScoreThreads = 256;
@@ -53,6 +56,7 @@ struct Workspace {
   double* hypE;        // [B][H][10][9]
   double* hypP;        // [B][H][10][12]
   double* hypP0;       // [B][H][12]
+  double* sstate;      // [kStateFields][B][H]: solve state between k_solve_front, k_roots, k_solve_back
   int32_t* cand_off;   // [B][H]
   int32_t* cand_total; // [64]
   double* candE;       // [B][Cmax][12]
@@ -75,6 +79,7 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   t.hypE = (double*)take(bc * H * kMaxSlots * 9 * 8);
   t.hypP = (double*)take(bc * H * kMaxSlots * 12 * 8);
   t.hypP0 = (double*)take(bc * H * 12 * 8);
+  t.sstate = (double*)take((size_t)kStateFields * bc * H * 8);
   t.cand_off = (int32_t*)take(bc * H * 4);
   t.cand_total = (int32_t*)take(SFM_MAX_BATCH * 4);
   t.candE = (double*)take(bc * C * kCandStride * 8);
@@ -139,30 +144,23 @@ struct FlowSrc {
 // Sturm iterations): only `lanes` lanes of each wave carry a hypothesis, so a
 // pair's 4096 hypotheses occupy 4096 / lanes waves and every CU has several
 // independent instruction streams to hide the scratch latency.
-#ifdef SFM_SOLVE_STATS
-// experiment builds only: summed cycles per solve phase (sample+load, basis,
-// equations, reduce, determinant, roots, E+cheirality) over all hypotheses
-__device__ unsigned long long g_solve_stats[8];
-extern "C" int sfm_experiment_solve_stats(unsigned long long* out8) {
-  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_solve_stats), 64) == hipSuccess ? 0 : 2;
-}
-#define SOLVE_T(i) do { const unsigned long long t_ = clock64(); atomicAdd(&g_solve_stats[i], t_ - t0_); t0_ = t_; } while (0)
-#else
-#define SOLVE_T(i) do {} while (0)
-#endif
+// The solve runs as three kernels so that each keeps a small live state:
+//   k_solve_front  sample, E basis, constraint equations, reduction, det poly
+//   k_roots        Sturm root isolation on a register-resident sequence
+//                  (88 % of the former single kernel's time was spent here,
+//                  waiting on scratch-resident coefficients)
+//   k_solve_back   E per root, cheirality, compaction
+// The state in between (116 doubles per hypothesis) is stored field-major.
+__device__ __forceinline__ double& st_at(double* st, size_t stride, int f, size_t hb) { return st[f * stride + hb]; }
 
 template <class Src>
-__global__ __launch_bounds__(64) void k_solve(const Src src, PairParams pp, int H, uint64_t seed, int cheir, int lanes,
-                                              int32_t* __restrict__ out_nroots, int32_t* __restrict__ out_ncand,
-                                              double* __restrict__ hypE, double* __restrict__ hypP) {
+__global__ __launch_bounds__(64) void k_solve_front(const Src src, PairParams pp, int H, uint64_t seed, int lanes,
+                                                    double* __restrict__ st, size_t stride) {
   const int b = blockIdx.y;
   if ((int)threadIdx.x >= lanes) return;
   const int h = blockIdx.x * lanes + threadIdx.x;
   if (h >= H) return;
   const int64_t n = pp.n[b];
-#ifdef SFM_SOLVE_STATS
-  unsigned long long t0_ = clock64();
-#endif
   int64_t idx[5];
   sample5(seed, (uint32_t)h, n, idx);
   double q[5][2], qp[5][2];
@@ -171,31 +169,101 @@ __global__ __launch_bounds__(64) void k_solve(const Src src, PairParams pp, int 
     const double4 v = src.load(b, idx[d]);
     q[d][0] = v.x; q[d][1] = v.y; qp[d][0] = v.z; qp[d][1] = v.w;
   }
-  SOLVE_T(0);
   Lin Eb[9];
   essential_basis(q, qp, Eb);
-  SOLVE_T(1);
   Eqs A;
   build_equations(Eb, A);
-  SOLVE_T(2);
   reduce_equations(A);
-  SOLVE_T(3);
   double poly[11];
   determinant_poly(A, poly);
-  SOLVE_T(4);
+  const size_t hb = (size_t)b * H + h;
+#pragma unroll
+  for (int e = 0; e < 9; ++e)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st_at(st, stride, kStEb + e * 4 + k, hb) = Eb[e].c[k];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      st_at(st, stride, kStA + i * 3 + j, hb) = A.e0[i][j];
+      st_at(st, stride, kStA + 9 + i * 3 + j, hb) = A.e1[i][j];
+      st_at(st, stride, kStA + 18 + i * 3 + j, hb) = A.e2[i][j];
+      st_at(st, stride, kStA + 27 + i * 3 + j, hb) = A.e3[i][j];
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) st_at(st, stride, kStA + 36 + i, hb) = A.e4[i];
+#pragma unroll
+  for (int d = 0; d < 5; ++d) {
+    st_at(st, stride, kStQ + 4 * d + 0, hb) = q[d][0];
+    st_at(st, stride, kStQ + 4 * d + 1, hb) = q[d][1];
+    st_at(st, stride, kStQ + 4 * d + 2, hb) = qp[d][0];
+    st_at(st, stride, kStQ + 4 * d + 3, hb) = qp[d][1];
+  }
+#pragma unroll
+  for (int i = 0; i <= 10; ++i) st_at(st, stride, kStPoly + i, hb) = poly[i];
+}
+
+__global__ __launch_bounds__(64) void k_roots(int H, int lanes, double* __restrict__ st, size_t stride,
+                                              int32_t* __restrict__ out_nroots) {
+  const int b = blockIdx.y;
+  if ((int)threadIdx.x >= lanes) return;
+  const int h = blockIdx.x * lanes + threadIdx.x;
+  if (h >= H) return;
+  const size_t hb = (size_t)b * H + h;
+  double poly[11];
+#pragma unroll
+  for (int i = 0; i <= 10; ++i) poly[i] = st_at(st, stride, kStPoly + i, hb);
   double roots[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) roots[i] = 0.0;
-  const int nr = real_roots(poly, roots);
-  SOLVE_T(5);
-  const int nv = nr > 0 ? (nr < 10 ? nr : 10) : 0;
+  const int nr = real_roots_r(poly, roots);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) st_at(st, stride, kStRoots + i, hb) = roots[i];
+  out_nroots[hb] = nr;
+}
+
+__global__ __launch_bounds__(64) void k_solve_back(int H, int cheir, const double* __restrict__ st, size_t stride,
+                                                   const int32_t* __restrict__ nroots,
+                                                   int32_t* __restrict__ out_ncand, double* __restrict__ hypE,
+                                                   double* __restrict__ hypP) {
+  const int b = blockIdx.y;
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
   const size_t hb = (size_t)b * H + h;
+  const int nr = nroots[hb];
+  const int nv = nr > 0 ? (nr < 10 ? nr : 10) : 0;
+  Lin Eb[9];
+#pragma unroll
+  for (int e = 0; e < 9; ++e)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Eb[e].c[k] = st[(kStEb + e * 4 + k) * stride + hb];
+  Eqs A;   // only the blocks compute_E_matrix reads
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      A.e0[i][j] = st[(kStA + i * 3 + j) * stride + hb];
+      A.e1[i][j] = st[(kStA + 9 + i * 3 + j) * stride + hb];
+      A.e2[i][j] = st[(kStA + 18 + i * 3 + j) * stride + hb];
+      A.e3[i][j] = st[(kStA + 27 + i * 3 + j) * stride + hb];
+    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) A.e4[i] = st[(kStA + 36 + i) * stride + hb];
+  double q[5][2], qp[5][2];
+#pragma unroll
+  for (int d = 0; d < 5; ++d) {
+    q[d][0] = st[(kStQ + 4 * d + 0) * stride + hb];
+    q[d][1] = st[(kStQ + 4 * d + 1) * stride + hb];
+    qp[d][0] = st[(kStQ + 4 * d + 2) * stride + hb];
+    qp[d][1] = st[(kStQ + 4 * d + 3) * stride + hb];
+  }
   double* Eo = hypE + hb * kMaxSlots * 9;
   double* Po = hypP + hb * kMaxSlots * 12;
   int nc = 0;
   for (int m = 0; m < nv; ++m) {
+    const double w = st[(kStRoots + m) * stride + hb];
     double E[9];
-    essential_at_root(Eb, A, roots[m], E);
+    essential_at_root(Eb, A, w, E);
     if (!cheir) {
 #pragma unroll
       for (int e = 0; e < 9; ++e) Eo[m * 9 + e] = E[e];
@@ -217,8 +285,6 @@ __global__ __launch_bounds__(64) void k_solve(const Src src, PairParams pp, int 
       for (int e = 0; e < 9; ++e) Eo[e] = E[e];
     }
   }
-  SOLVE_T(6);
-  out_nroots[hb] = nr;
   out_ncand[hb] = nc;
 }
 
@@ -998,9 +1064,13 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   {
     ProfScope ps("ransac_solve", s);
     const int lanes = tuning().solve_lanes;
-    hipLaunchKernelGGL(k_solve<Src>, dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H, seed, cheir,
-                       lanes,
-                       w.nroots, w.ncand, w.hypE, w.hypP);
+    const size_t stride = (size_t)bc * H;
+    hipLaunchKernelGGL(k_solve_front<Src>, dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H, seed,
+                       lanes, w.sstate, stride);
+    hipLaunchKernelGGL(k_roots, dim3((H + tuning().roots_lanes - 1) / tuning().roots_lanes, bc), dim3(64), 0, s, H,
+                       tuning().roots_lanes, w.sstate, stride, w.nroots);
+    hipLaunchKernelGGL(k_solve_back, dim3((H + 63) / 64, bc), dim3(64), 0, s, H, cheir, w.sstate, stride, w.nroots,
+                       w.ncand, w.hypE, w.hypP);
   }
   SFM_LAUNCHED();
   const bool fast = thr >= 0x1p-40 && thr < 1.0;

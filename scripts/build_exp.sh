@@ -1,12 +1,18 @@
 #!/bin/bash
-# Experiment variants of libsfm_hip.so (score-kernel statistics / no-fallback
-# timing) into scripts/exp/, same flags as csrc/Makefile.  Never used by the
-# product; selected with SFM_HIP_LIB by scripts/score_experiment.py.
+# Experiment variants of libsfm_hip.so into scripts/exp/ (same flags as
+# csrc/Makefile); never used by the product, selected with SFM_HIP_LIB:
+#   STATS       score-kernel undecided statistics   (scripts/score_experiment.py)
+#   NOFALLBACK  score kernel without the float64 re-tests (timing only; wrong counts)
+#   SOLVESTATS  per-phase cycle counters of k_solve  (scripts/solve_experiment.py)
 set -e
 cd "$(dirname "$0")/../deep-sfm-revisited_amd/csrc"
 mkdir -p ../../scripts/exp
-for v in STATS NOFALLBACK; do
+build() {
+  local name=$1; shift
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -fPIC -shared \
-        -I../../include -Wno-unused-result -DSFM_SCORE_$v -o ../../scripts/exp/libsfm_hip_$v.so \
+        -I../../include -Wno-unused-result "$@" -o ../../scripts/exp/libsfm_hip_$name.so \
         capi.hip ransac5.hip sweep.hip depth.hip irls.hip host_polish.cpp
-done
+}
+build STATS -DSFM_SCORE_STATS
+build NOFALLBACK -DSFM_SCORE_NOFALLBACK
+build SOLVESTATS -DSFM_SOLVE_STATS
