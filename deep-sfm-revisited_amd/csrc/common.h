@@ -12,7 +12,7 @@ void set_error(const std::string& msg);
 // Launch-shape tuning knobs (sfm_tune_set); read by the launchers.
 struct Tuning {
   int solve_lanes = 32;          // active lanes per k_solve_front wave (1..64)
-  int roots_lanes = 64;          // active lanes per k_roots wave (1..64)
+  int roots_lanes = 32;          // active lanes per k_roots wave (1..64)
   int sweep_items_per_block = 4; // consecutive (row, plane, window) items per sweep block
   int sweep_lane_pixels = 0;     // 1: warped lanes own 4 consecutive pixels (16-byte stores)
   int score_blocks_per_cu = 32;  // persistent score grid
