@@ -40,8 +40,9 @@ constexpr int kKC = 32;           // candidates per score tile
 constexpr int kPPL = 8;           // points per lane per chunk
 constexpr int kScoreThreads = 256;
 constexpr int kChunk = kScoreThreads * kPPL;
-constexpr int kChunksPerItem = 4;
-constexpr int kPtsPerItem = kChunk * kChunksPerItem;   // 8192
+constexpr int kPPL32 = 8;          // points per lane per chunk in k_score32 (6, 10, 12 measured slower)
+constexpr int kPtsPerItem = 8192;  // points per k_score item (a whole number of chunks)
+static_assert(kPtsPerItem % kChunk == 0, "item = whole chunks");
 
 struct PairParams {
   int64_t n[SFM_MAX_BATCH];
@@ -323,14 +324,17 @@ __device__ __forceinline__ double guard_constant(const double* E, double g) {
 // 8.02 u R M by the standard bounds; the reference's own float64 error is far
 // below the slack).  Bounding the cross terms 2|a|alpha and 2 sqrt(D) beta by
 // AM-GM with weight 2^7 turns the reference test into two sign tests:
-//     inlier  if fma(-t2lo, D, fma(a, a,  eps1)) < 0
-//     outlier if fma(-t2hi, D, fma(a, a, -eps2)) > 0
+//     inlier  if fma(-t2lo, D, a*a) < -eps1
+//     outlier if fma(-t2hi, D, a*a) >  eps2
 //     eps1 = 129 alpha^2 + 128 thr^2 beta^2           = A1 M^4 + B1 M^2
 //     eps2 = (128 alpha^2 + 129 thr^2 beta^2)/(1-2^-7) = A2 M^4 + B2 M^2
 //     t2lo = thr^2 (1 - 2^-6 - 2^-19),  t2hi = thr^2 (1 + 2^-7)/(1 - 2^-7) (1 + 2^-19)
-// (derivation in DESIGN.md, "Scoring").  Anything else is undecided and
-// re-evaluated by the float64 path.  A*, B* carry a 2^-20 upward slack that
-// covers their float32 rounding and the three float32 operations forming eps.
+// (rounding is monotone and +-eps are floats, so each compare implies the
+// exact inequality on aa = fl(a^2); aa is within u of a^2, the same loss as
+// rounding a^2 + eps once; derivation in DESIGN.md, "Scoring").  Anything else
+// is undecided and re-evaluated by the float64 path.  A*, B* carry a 2^-20
+// upward slack that covers their float32 rounding and the float32 operations
+// forming eps; slots 14/15 hold -eps1 and eps2 at M = 1 (the common case).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void fp32_constants(const double* E, double thr, bool enable, float* out) {
   double R = 0.0;
@@ -346,11 +350,15 @@ __device__ __forceinline__ void fp32_constants(const double* E, double thr, bool
   const double al = 8.0 * 0x1p-24 * R * (1.0 + 0x1p-20) + 0x1p-120;
   const double be = 8.1 * 0x1p-24 * R * (1.0 + 0x1p-20) + 0x1p-120;
   const double t2 = thr * thr, up = 1.0 + 0x1p-20;
-  out[9] = ok ? (float)(129.0 * al * al * up) : 0.0f;
-  out[10] = ok ? (float)(128.0 * t2 * be * be * up) : 0.0f;
-  out[11] = ok ? (float)(128.0 * al * al / (1.0 - 0x1p-7) * up) : 0.0f;
-  out[12] = ok ? (float)(129.0 * t2 * be * be / (1.0 - 0x1p-7) * up) : 0.0f;
+  const double A1 = 129.0 * al * al * up, B1 = 128.0 * t2 * be * be * up;
+  const double A2 = 128.0 * al * al / (1.0 - 0x1p-7) * up, B2 = 129.0 * t2 * be * be / (1.0 - 0x1p-7) * up;
+  out[9] = ok ? (float)A1 : 0.0f;
+  out[10] = ok ? (float)B1 : 0.0f;
+  out[11] = ok ? (float)A2 : 0.0f;
+  out[12] = ok ? (float)B2 : 0.0f;
   out[13] = ok ? 1.0f : 0.0f;
+  out[14] = ok ? -(float)((A1 + B1) * up) : 0.0f;
+  out[15] = ok ? (float)((A2 + B2) * up) : 0.0f;
 }
 
 // ---------------------------------------------------------------------------
@@ -503,6 +511,13 @@ __device__ __forceinline__ bool inlier_test(const double* E, const Addends& ad, 
   return in;
 }
 
+// Level-3 test (reference order), kept as a named call site for the drain.
+__device__ __forceinline__
+bool inlier_reference_call(const double* E, double x, double y, double xp, double yp,
+                                                   double thr) {
+  return inlier_reference(E, x, y, xp, yp, thr);
+}
+
 // One chunk (kPPL points per lane) against the tile's nc candidates.  One
 // ballot per (candidate, point); the num_test / num_ransac_test prefixes are
 // applied as precomputed wave masks (SAME: both prefixes equal, one count).
@@ -609,201 +624,246 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const Src src, PairPara
 
 // ---------------------------------------------------------------------------
 // Phase 3b: scoring with the float32 pre-decision (fp32_constants).
-// Same work decomposition as k_score; only float32 copies of the points stay
-// in registers.  (Plain v_fma_f32 issues at twice the fp64 rate on gfx950;
-// packed v_pk_fma_f32 measured no faster.)  Undecided lanes and the rare
-// chunks with a coordinate beyond +-1 reload their points and take the
-// float64 test.
+// Only float32 copies of the points stay in registers.  (Plain v_fma_f32
+// issues at twice the fp64 rate on gfx950; packed v_pk_fma_f32 measured no
+// faster.)  The kernel sits at the measured VALU issue ceiling
+// (scripts/probe_vgpr_bank.hip: ~1.15-1.3 ns per wave-FMA per SIMD at 4-8
+// waves), so its cost is its VALU count: 21 per evaluation in the common
+// path.  Undecided evaluations and lanes with a coordinate beyond 2^12 are
+// queued and re-tested in float64.
 // ---------------------------------------------------------------------------
 
-// wave-uniform pointer kept in SGPRs (the compiler cannot prove uniformity of
-// values derived from the LDS pair search)
-template <typename Tp>
-__device__ __forceinline__ const Tp* uniform_ptr(const Tp* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return reinterpret_cast<const Tp*>(((uint64_t)hi << 32) | lo);
-}
-
 #ifdef SFM_SCORE_STATS
-// experiment builds only (scripts/score_experiment.py): pair-iterations,
-// pair-iterations with an undecided lane, undecided lane-evaluations
+// experiment builds only (scripts/score_experiment.py): (candidate, point
+// slot) wave iterations, those with an undecided lane, undecided evaluations
 __device__ unsigned long long g_score_stats[3];
 extern "C" int sfm_experiment_score_stats(unsigned long long* out3) {
   return hipMemcpyFromSymbol(out3, HIP_SYMBOL(g_score_stats), 24) == hipSuccess ? 0 : 2;
 }
 #endif
 
-// float64 decision of one point (reloaded); guard per point (any scale)
-template <class Src>
-__device__ __forceinline__ bool inlier_f64(const double* __restrict__ Ec, const Src& src, int b, int p,
-                                           const ScoreConsts& kc) {
-  const double4 v = src.load(b, p);
+// float64 decision of one (reloaded) point; guard per point (any scale)
+__device__ __forceinline__ bool inlier_f64v(const double* __restrict__ Ec, const double4 v, const ScoreConsts& kc) {
   double E[9];
 #pragma unroll
   for (int e = 0; e < 9; ++e) E[e] = Ec[e];
-  const Addends ad{E[2], E[5], E[8], E[6], E[7]};
-  return inlier_test<true, false>(E, ad, Ec[9], v.x, v.y, v.z, v.w, point_scale(v.x, v.y, v.z, v.w), kc);
+  const double x = v.x, y = v.y, xp = v.z, yp = v.w;
+  const double ex0 = fma(E[0], x, fma(E[1], y, E[2]));
+  const double ex1 = fma(E[3], x, fma(E[4], y, E[5]));
+  const double ex2 = fma(E[6], x, fma(E[7], y, E[8]));
+  const double xe0 = fma(xp, E[0], fma(yp, E[3], E[6]));
+  const double xe1 = fma(xp, E[1], fma(yp, E[4], E[7]));
+  const double a = fma(xp, ex0, fma(yp, ex1, ex2));
+  const double D = fma(xe1, xe1, fma(xe0, xe0, fma(ex1, ex1, ex0 * ex0)));
+  const double lhs = a * a;
+  const bool g = D >= Ec[9] * point_scale(x, y, xp, yp);
+  const bool fin = g && (lhs < kc.t2lo * D);
+  const bool fout = g && (lhs > kc.t2hi * D);
+  if (fin || fout) return fin;
+  return inlier_reference_call(E, x, y, xp, yp, kc.thr);
 }
 
-// Float32 pass of one chunk.  Every decision is a wave mask straight out
-// of one compare (inlier: din < 0, outlier: dout > 0; both finite here since
-// the chunk's coordinates are within +-1 and the candidate passed ok32), so
-// the bookkeeping is scalar: counts by popcount, undecided = ~(in | out) per
-// point.  Undecided points are re-tested in float64 after the unrolled loop.
-constexpr int kQueue = 1024;   // undecided (candidate, point) entries per wave (LDS)
+// Float32 pass.  Every decision is a wave mask straight out of one compare
+// (inlier: din < -eps1, outlier: dout > eps2; all finite here since the
+// lane's coordinates are within 2^12 and the candidate passed ok32), so the
+// bookkeeping is scalar: counts by popcount, undecided = ~(in | out) per
+// point.  Undecided points are queued and re-tested in float64.
 
-template <bool SAME, bool MASKED, class Src>
-__device__ __forceinline__ void score32_chunk(const double* __restrict__ CE, int nc, const Src& src, int b,
-                                              int cb, int tid, int p1, int T, int R, const float (&x)[kPPL],
-                                              const float (&y)[kPPL], const float (&xp)[kPPL],
-                                              const float (&yp)[kPPL], const uint64_t (&mT)[kPPL],
-                                              const uint64_t (&mR)[kPPL], float M2, uint64_t bad,
-                                              const ScoreConsts& kc, int lane, int32_t (*cnt)[2], uint32_t* q) {
+// Lanes [0, n) of a wave (n may lie outside [0, 64]).
+__device__ __forceinline__ uint64_t lane_prefix(int n) {
+  return n >= 64 ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1ull));
+}
+
+constexpr int kQueue = 1024;        // undecided (candidate, point) entries per wave (LDS)
+static_assert(kQueue >= 64 * kPPL32, "the queue takes one candidate's undecided points past its low mark");
+
+// Append the wave's undecided lanes (mask und) of one point slot to the queue.
+__device__ __forceinline__ void enqueue_undecided(uint64_t und, int c, int p, int lane, uint32_t* q, int& qn) {
+#ifdef SFM_SCORE_STATS
+  if (lane == 0) {
+    atomicAdd(&g_score_stats[0], 1ull);
+    if (und) atomicAdd(&g_score_stats[1], 1ull);
+    atomicAdd(&g_score_stats[2], (unsigned long long)__popcll(und));
+  }
+#endif
+#ifndef SFM_SCORE_NOFALLBACK
+  if (!und) return;                                     // wave-uniform
+  if ((und >> lane) & 1ull) {
+    const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(und >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)und, 0));
+    q[pos] = ((uint32_t)c << 24) | (uint32_t)p;
+  }
+  qn += __popcll(und);
+#endif
+}
+
+// One float32 pass of a wave over candidates [c, nc) of its chunk (lane l
+// holds points cb + 64k + l).  Returns the first candidate not processed: nc,
+// or one met with the queue past its low mark (the caller drains the queue,
+// reloads the chunk and resumes there).  The float64 test stays out of this
+// loop so that its registers stay out of the hot loop's footprint.
+//   MASKED: the chunk crosses the num_test (nT) or num_ransac_test (nR)
+//   prefix, counted from the chunk base; SAME: both prefixes are equal.
+//   GEN: some lane has M != 1 or is bad; otherwise eps are the records'
+//   precomputed M = 1 values.
+template <bool SAME, bool MASKED, bool GEN>
+__device__ __forceinline__ int score32_pass(const double* __restrict__ CE, int c, int nc, int pl, int nT, int nR,
+                                            const float (&x)[kPPL32], const float (&y)[kPPL32],
+                                            const float (&xp)[kPPL32], const float (&yp)[kPPL32], float M2,
+                                            uint64_t bad, const ScoreConsts& kc, int lane, int32_t (*cnt)[2],
+                                            uint32_t* q, int& qn) {
   const float nt2lo = -kc.t2lo32, nt2hi = -kc.t2hi32;
   const float M4 = M2 * M2;
-  int qn = 0;
-  for (int c = 0; c < nc; ++c) {
-    const double* Ec = CE + (size_t)c * kCandStride;     // the tile's records, staged in LDS
-    const float* F = reinterpret_cast<const float*>(Ec + 10);
+  for (; c < nc; ++c) {
+    if (qn > kQueue - 64 * kPPL32) break;               // drain first
+    const float* F = reinterpret_cast<const float*>(CE + (size_t)c * kCandStride + 10);
     int sT = 0, sR = 0;
-    uint64_t und[kPPL];
-    if (F[13] != 0.0f) {
+    uint64_t undk[kPPL32];
+    if (__builtin_amdgcn_readfirstlane(__float_as_uint(F[13])) != 0u) {   // ok32 (wave-uniform: 1.0f or 0.0f)
       const float e0 = F[0], e1 = F[1], e2 = F[2], e3 = F[3], e4 = F[4], e5 = F[5], e6 = F[6], e7 = F[7], e8 = F[8];
-      const float eps1 = __builtin_fmaf(F[9], M4, F[10] * M2);      // per lane: its points' M
-      const float neps2 = -__builtin_fmaf(F[11], M4, F[12] * M2);
-      // stage by stage across the kPPL points: independent FMA chains
-      float ex0[kPPL], ex1[kPPL], ex2[kPPL], xe0[kPPL], xe1[kPPL], a[kPPL], D[kPPL], din[kPPL], dout[kPPL];
+      float neps1, eps2;
+      if (GEN) {
+        neps1 = -__builtin_fmaf(F[9], M4, F[10] * M2);               // per lane: its points' M
+        eps2 = __builtin_fmaf(F[11], M4, F[12] * M2);
+      } else {
+        neps1 = F[14];
+        eps2 = F[15];
+      }
+      // stage by stage across the kPPL32 points: independent FMA chains
+      float ex0[kPPL32], ex1[kPPL32], ex2[kPPL32], xe0[kPPL32], xe1[kPPL32], a[kPPL32], D[kPPL32], aa[kPPL32];
+      float din[kPPL32], dout[kPPL32];
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) ex0[k] = __builtin_fmaf(e0, x[k], __builtin_fmaf(e1, y[k], e2));
+      for (int k = 0; k < kPPL32; ++k) ex0[k] = __builtin_fmaf(e0, x[k], __builtin_fmaf(e1, y[k], e2));
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) ex1[k] = __builtin_fmaf(e3, x[k], __builtin_fmaf(e4, y[k], e5));
+      for (int k = 0; k < kPPL32; ++k) ex1[k] = __builtin_fmaf(e3, x[k], __builtin_fmaf(e4, y[k], e5));
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) ex2[k] = __builtin_fmaf(e6, x[k], __builtin_fmaf(e7, y[k], e8));
+      for (int k = 0; k < kPPL32; ++k) ex2[k] = __builtin_fmaf(e6, x[k], __builtin_fmaf(e7, y[k], e8));
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) xe0[k] = __builtin_fmaf(xp[k], e0, __builtin_fmaf(yp[k], e3, e6));
+      for (int k = 0; k < kPPL32; ++k) xe0[k] = __builtin_fmaf(xp[k], e0, __builtin_fmaf(yp[k], e3, e6));
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) xe1[k] = __builtin_fmaf(xp[k], e1, __builtin_fmaf(yp[k], e4, e7));
+      for (int k = 0; k < kPPL32; ++k) xe1[k] = __builtin_fmaf(xp[k], e1, __builtin_fmaf(yp[k], e4, e7));
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) a[k] = __builtin_fmaf(xp[k], ex0[k], __builtin_fmaf(yp[k], ex1[k], ex2[k]));
+      for (int k = 0; k < kPPL32; ++k) a[k] = __builtin_fmaf(xp[k], ex0[k], __builtin_fmaf(yp[k], ex1[k], ex2[k]));
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k)
+      for (int k = 0; k < kPPL32; ++k)
         D[k] = __builtin_fmaf(xe1[k], xe1[k], __builtin_fmaf(xe0[k], xe0[k], __builtin_fmaf(ex1[k], ex1[k], ex0[k] * ex0[k])));
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) din[k] = __builtin_fmaf(nt2lo, D[k], __builtin_fmaf(a[k], a[k], eps1));
+      for (int k = 0; k < kPPL32; ++k) aa[k] = a[k] * a[k];
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) dout[k] = __builtin_fmaf(nt2hi, D[k], __builtin_fmaf(a[k], a[k], neps2));
+      for (int k = 0; k < kPPL32; ++k) din[k] = __builtin_fmaf(nt2lo, D[k], aa[k]);
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) {
-        const uint64_t mi = __ballot(din[k] < 0.0f) & ~bad;
-        const uint64_t mo = __ballot(dout[k] > 0.0f);
-        und[k] = ~(mi | mo) | bad;
+      for (int k = 0; k < kPPL32; ++k) dout[k] = __builtin_fmaf(nt2hi, D[k], aa[k]);
+#pragma unroll
+      for (int k = 0; k < kPPL32; ++k) {
+        uint64_t mi = __ballot(din[k] < neps1);
+        const uint64_t mo = __ballot(dout[k] > eps2);
+        uint64_t und = ~(mi | mo);
+        if (GEN) {
+          mi &= ~bad;
+          und |= bad;
+        }
         if (MASKED) {
-          und[k] &= mT[k] | mR[k];
-          sT += __popcll(mi & mT[k]);
-          if (!SAME) sR += __popcll(mi & mR[k]);
+          const uint64_t mT = lane_prefix(nT - 64 * k), mR = lane_prefix(nR - 64 * k);
+          und &= mT | mR;
+          sT += __popcll(mi & mT);
+          if (!SAME) sR += __popcll(mi & mR);
         } else {
           sT += __popcll(mi);
         }
+        undk[k] = und;
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) und[k] = MASKED ? (mT[k] | mR[k]) : ~0ull;   // candidate outside the float32 range
+      for (int k = 0; k < kPPL32; ++k)                  // candidate outside the float32 range
+        undk[k] = MASKED ? (lane_prefix(nT - 64 * k) | lane_prefix(nR - 64 * k)) : ~0ull;
     }
-#ifdef SFM_SCORE_STATS
-    {
-      uint64_t any = 0;
-      int n = 0;
+    // enqueue after the unrolled compares (enqueueing inside them splits the
+    // FMA block per point and costs SGPRs)
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) { any |= und[k]; n += __popcll(und[k]); }
-      if (lane == 0) {
-        atomicAdd(&g_score_stats[0], 1ull);
-        if (any) atomicAdd(&g_score_stats[1], 1ull);
-        atomicAdd(&g_score_stats[2], (unsigned long long)n);
-      }
-    }
-#endif
-#ifndef SFM_SCORE_NOFALLBACK
-    int nund = 0;
-#pragma unroll
-    for (int k = 0; k < kPPL; ++k) nund += __popcll(und[k]);
-    if (nund) {
-      if (qn + nund <= kQueue) {
-        // queue (candidate, point) for the compacted float64 pass after the loop
-#pragma unroll
-        for (int k = 0; k < kPPL; ++k) {
-          if (!und[k]) continue;                          // wave-uniform
-          if ((und[k] >> lane) & 1ull) {
-            const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(und[k] >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)und[k], 0));
-            q[pos] = ((uint32_t)c << 24) | (uint32_t)(cb + k * kScoreThreads + tid);
-          }
-          qn += __popcll(und[k]);
-        }
-      } else {
-        // queue full: float64 test now, one point per lane per round
-#pragma unroll 1
-        for (int k = 0; k < kPPL; ++k) {
-          if (!und[k]) continue;
-          const int p = cb + k * kScoreThreads + tid;
-          bool in = false;
-          if ((und[k] >> lane) & 1ull) in = inlier_f64(Ec, src, b, p, kc);
-          const uint64_t m = __ballot(in);
-          if (MASKED) {
-            sT += __popcll(m & mT[k]);
-            if (!SAME) sR += __popcll(m & mR[k]);
-          } else {
-            sT += __popcll(m);
-          }
-        }
-      }
-    }
-#endif
+    for (int k = 0; k < kPPL32; ++k) enqueue_undecided(undk[k], c, pl + 64 * k, lane, q, qn);
     if (SAME || !MASKED) sR = sT;
     if (lane == 0) {
       cnt[c][0] += sT;
       cnt[c][1] += sR;
     }
   }
-  // compacted float64 pass over the queued evaluations (64 per round)
+  return c;
+}
+
+// Compacted float64 pass over the queued evaluations: 64 lanes x kDrainBatch
+// entries per round, the point loads of a round issued together.
+constexpr int kDrainBatch = 4;
+
+template <class Src>
+__device__ __forceinline__ void score32_drain(const double* __restrict__ CE, const Src& src, int b, int T, int R,
+                                              const ScoreConsts& kc, int lane, int32_t (*cnt)[2],
+                                              const uint32_t* q, int qn) {
 #pragma unroll 1
-  for (int i = lane; i < qn; i += 64) {
-    const uint32_t e = q[i];
-    const int c = (int)(e >> 24), p = (int)(e & 0xffffffu);
-    if (inlier_f64(CE + (size_t)c * kCandStride, src, b, p, kc)) {
-      if (p < T) atomicAdd(&cnt[c][0], 1);
-      if (p < R) atomicAdd(&cnt[c][1], 1);
+  for (int i0 = 0; i0 < qn; i0 += 64 * kDrainBatch) {
+    uint32_t e[kDrainBatch];
+    double4 v[kDrainBatch];
+#pragma unroll
+    for (int j = 0; j < kDrainBatch; ++j) {
+      const int i = i0 + 64 * j + lane;
+      e[j] = i < qn ? q[i] : 0xffffffffu;
+      v[j] = src.load(b, e[j] != 0xffffffffu ? (int)(e[j] & 0xffffffu) : 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kDrainBatch; ++j) {
+      if (e[j] == 0xffffffffu) continue;
+      const int c = (int)(e[j] >> 24), p = (int)(e[j] & 0xffffffu);
+      if (inlier_f64v(CE + (size_t)c * kCandStride, v[j], kc)) {
+        if (p < T) atomicAdd(&cnt[c][0], 1);
+        if (p < R) atomicAdd(&cnt[c][1], 1);
+      }
     }
   }
 }
 
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Work unit: one wave scores one (pair, 32-candidate tile, kPtsPerWave-point
+// span) item on its own -- its own LDS copy of the tile's records, counts and
+// queue, no block barrier -- so a wave that drains a long queue never holds up
+// the other waves of its block.  The queue collects the whole item's
+// undecided evaluations (drained at the item's end, or earlier when past its
+// low mark), so drains run in full 64-lane rounds.
+constexpr int kPtsPerWave = kPPL32 * 64 * 4;
+
 template <class Src>
-__global__ __launch_bounds__(kScoreThreads) void k_score32(const Src src, PairParams pp, int batch, int cmax,
-                                                           const int32_t* __restrict__ cand_total,
-                                                           const double* __restrict__ candE,
-                                                           int32_t* __restrict__ cntT, int32_t* __restrict__ cntR,
-                                                           ScoreConsts kc) {
-  __shared__ int32_t s_cnt[kScoreThreads / 64][kKC][2];
+__global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
+               const double* __restrict__ candE, int32_t* __restrict__ cntT, int32_t* __restrict__ cntR,
+               ScoreConsts kc) {
+  constexpr int kWaves = kScoreThreads / 64;
+  __shared__ int32_t s_cnt[kWaves][kKC][2];
   __shared__ int32_t s_items[SFM_MAX_BATCH + 1];
   __shared__ int32_t s_tiles[SFM_MAX_BATCH];
-  __shared__ double s_cand[kKC * kCandStride];
-  __shared__ uint32_t s_queue[kScoreThreads / 64][kQueue];
+  __shared__ double2 s_cand[kWaves][kKC * kCandStride / 2];
+  __shared__ uint32_t s_queue[kWaves][kQueue];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) {
     int acc = 0;
     for (int b = 0; b < batch; ++b) {
       const int tiles = (cand_total[b] + kKC - 1) / kKC;
+      const int splits = (max(pp.test[b], pp.rtest[b]) + kPtsPerWave - 1) / kPtsPerWave;
       s_tiles[b] = tiles;
       s_items[b] = acc;
-      acc += tiles * pp.splits[b];
+      acc += tiles * splits;
     }
     s_items[batch] = acc;
   }
-  for (int i = tid; i < (kScoreThreads / 64) * kKC * 2; i += kScoreThreads) (&s_cnt[0][0][0])[i] = 0;
+  for (int i = tid; i < kWaves * kKC * 2; i += kScoreThreads) (&s_cnt[0][0][0])[i] = 0;
   __syncthreads();
+  int32_t(*cnt)[2] = s_cnt[wv];
+  uint32_t* queue = s_queue[wv];
+  const double* CE = reinterpret_cast<const double*>(s_cand[wv]);
   const int total = __builtin_amdgcn_readfirstlane(s_items[batch]);
-  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
+  for (int item = gw; item < total; item += gridDim.x * kWaves) {
     int b = 0;
     while (item >= s_items[b + 1]) ++b;
     b = __builtin_amdgcn_readfirstlane(b);                      // wave-uniform (LDS-derived)
@@ -815,55 +875,67 @@ __global__ __launch_bounds__(kScoreThreads) void k_score32(const Src src, PairPa
     const int nc = min(kKC, ctot - c0);
     const int T = pp.test[b], R = pp.rtest[b];
     const int M = max(T, R);
-    const int p0 = split * kPtsPerItem;
-    const int p1 = min(M, p0 + kPtsPerItem);
+    const int p0 = split * kPtsPerWave;
+    const int p1 = min(M, p0 + kPtsPerWave);
     {
-      // stage the tile's candidate records (nc x 128 B) in LDS
-      const double2* src = reinterpret_cast<const double2*>(candE + ((size_t)b * cmax + c0) * kCandStride);
-      double2* dst = reinterpret_cast<double2*>(s_cand);
-      for (int i = tid; i < nc * (kCandStride / 2); i += kScoreThreads) dst[i] = src[i];
+      // this wave's copy of the tile's candidate records (nc x 144 B)
+      const double2* srcc = reinterpret_cast<const double2*>(candE + ((size_t)b * cmax + c0) * kCandStride);
+      for (int i = lane; i < nc * (kCandStride / 2); i += 64) s_cand[wv][i] = srcc[i];
     }
-    __syncthreads();
-    const double* CE = s_cand;
-    for (int cb = p0; cb < p1; cb += kChunk) {
-      float x[kPPL], y[kPPL], xp[kPPL], yp[kPPL];
-      uint64_t mT[kPPL], mR[kPPL];
-      double M = 1.0;
+    wave_sync();
+    int qn = 0;
+    for (int cb = p0; cb < p1; cb += 64 * kPPL32) {
+      int c = 0;
+      for (;;) {
+        // (re)load the chunk: the points are dead while the queue drains
+        float x[kPPL32], y[kPPL32], xp[kPPL32], yp[kPPL32];
+        double Mx = 1.0;
+        const int pl = cb + lane;
 #pragma unroll
-      for (int k = 0; k < kPPL; ++k) {
-        const int p = cb + k * kScoreThreads + tid;
-        const double4 v = src.load(b, min(p, p1 - 1));
-        M = fmax(M, fmax(fmax(fabs(v.x), fabs(v.y)), fmax(fabs(v.z), fabs(v.w))));
-        x[k] = (float)v.x; y[k] = (float)v.y; xp[k] = (float)v.z; yp[k] = (float)v.w;
-        mT[k] = __ballot(p < p1 && p < T);
-        mR[k] = __ballot(p < p1 && p < R);
-      }
-      // lanes with a coordinate beyond 2^12 (or NaN) take the float64 test for all their points
-      const bool lane_bad = !(M <= 0x1p12);
-      const uint64_t bad = __ballot(lane_bad);
-      const float Mf = lane_bad ? 1.0f : (float)M;
-      const float M2 = Mf * Mf;
-      const bool full = cb + kChunk <= min(T, R);                 // no prefix masking needed
-      if (full) {
-        score32_chunk<true, false>(CE, nc, src, b, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
-                                   s_cnt[wv], s_queue[wv]);
-      } else if (T == R) {
-        score32_chunk<true, true>(CE, nc, src, b, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
-                                  s_cnt[wv], s_queue[wv]);
-      } else {
-        score32_chunk<false, true>(CE, nc, src, b, cb, tid, p1, T, R, x, y, xp, yp, mT, mR, M2, bad, kc, lane,
-                                   s_cnt[wv], s_queue[wv]);
+        for (int k = 0; k < kPPL32; ++k) {
+          const double4 v = src.load(b, min(pl + 64 * k, p1 - 1));
+          Mx = fmax(Mx, fmax(fmax(fabs(v.x), fabs(v.y)), fmax(fabs(v.z), fabs(v.w))));
+          x[k] = (float)v.x; y[k] = (float)v.y; xp[k] = (float)v.z; yp[k] = (float)v.w;
+        }
+        // lanes with a coordinate beyond 2^12 (or NaN) take the float64 test for all their points
+        const bool lane_bad = !(Mx <= 0x1p12);
+        const uint64_t bad = __ballot(lane_bad);
+        const bool unit = __ballot(Mx != 1.0) == 0;                  // every lane M = 1, none bad
+        const float Mf = lane_bad ? 1.0f : (float)Mx;
+        const float M2 = Mf * Mf;
+        const int nT = min(p1, T) - cb, nR = min(p1, R) - cb;
+        if (min(nT, nR) >= 64 * kPPL32) {                           // no prefix masking needed
+          if (unit) c = score32_pass<true, false, false>(CE, c, nc, pl, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
+          else c = score32_pass<true, false, true>(CE, c, nc, pl, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
+        } else if (T == R) {
+          c = score32_pass<true, true, true>(CE, c, nc, pl, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
+        } else {
+          c = score32_pass<false, true, true>(CE, c, nc, pl, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
+        }
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (c >= nc) break;
+#ifndef SFM_SCORE_NOFALLBACK
+        wave_sync();                                      // queue past its low mark: drain, resume at c
+        score32_drain(CE, src, b, T, R, kc, lane, cnt, queue, qn);
+        qn = 0;
+        wave_sync();
+#endif
       }
     }
-    __syncthreads();
-    if (tid < nc * 2) {
-      const int c = tid >> 1, which = tid & 1;
-      int s = 0;
-#pragma unroll
-      for (int w = 0; w < kScoreThreads / 64; ++w) { s += s_cnt[w][c][which]; s_cnt[w][c][which] = 0; }
-      if (s) atomicAdd((which ? cntR : cntT) + (size_t)b * cmax + c0 + c, s);
+#ifndef SFM_SCORE_NOFALLBACK
+    wave_sync();
+    score32_drain(CE, src, b, T, R, kc, lane, cnt, queue, qn);
+#endif
+    wave_sync();
+    {
+      const int c = lane >> 1, which = lane & 1;
+      if (c < nc) {
+        const int s = cnt[c][which];
+        cnt[c][which] = 0;
+        if (s) atomicAdd((which ? cntR : cntT) + (size_t)b * cmax + c0 + c, s);
+      }
     }
-    __syncthreads();
+    wave_sync();
   }
 }
 

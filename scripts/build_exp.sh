@@ -1,9 +1,11 @@
 #!/bin/bash
 # Experiment variants of libsfm_hip.so into scripts/exp/ (same flags as
-# csrc/Makefile); never used by the product, selected with SFM_HIP_LIB:
+# csrc/Makefile); never used by the product, selected with SFM_HIP_LIB.
+# With no arguments builds the standard set:
 #   STATS       score-kernel undecided statistics   (scripts/score_experiment.py)
 #   NOFALLBACK  score kernel without the float64 re-tests (timing only; wrong counts)
 #   SOLVESTATS  per-phase cycle counters of k_solve  (scripts/solve_experiment.py)
+# or NAME=FLAGS pairs, e.g.  scripts/build_exp.sh "P6W6=-DSFM_PPL32=6 -DSFM_SCORE_WAVES=6"
 set -e
 cd "$(dirname "$0")/../deep-sfm-revisited_amd/csrc"
 mkdir -p ../../scripts/exp
@@ -13,6 +15,15 @@ build() {
         -I../../include -Wno-unused-result "$@" -o ../../scripts/exp/libsfm_hip_$name.so \
         capi.hip ransac5.hip sweep.hip depth.hip irls.hip host_polish.cpp
 }
-build STATS -DSFM_SCORE_STATS
-build NOFALLBACK -DSFM_SCORE_NOFALLBACK
-build SOLVESTATS -DSFM_SOLVE_STATS
+if [ $# -eq 0 ]; then
+  build STATS -DSFM_SCORE_STATS
+  build NOFALLBACK -DSFM_SCORE_NOFALLBACK
+  build SOLVESTATS -DSFM_SOLVE_STATS
+else
+  for spec in "$@"; do
+    name=${spec%%=*}; flags=${spec#*=}
+    # shellcheck disable=SC2086
+    build "$name" $flags &
+  done
+  wait
+fi

@@ -25,5 +25,6 @@ lib = _lib.load()
 if hasattr(lib, "sfm_experiment_score_stats"):
     out = (ctypes.c_ulonglong * 3)()
     lib.sfm_experiment_score_stats(out)
-    print("pair-iterations", out[0], "with undecided lane", out[1], "frac %.4f" % (out[1] / max(out[0], 1)),
-          "undecided lane-evals", out[2], "per eval %.6f" % (out[2] / max(out[0] * 128, 1)))
+    print("(candidate, point-slot) wave iterations", out[0], "with an undecided lane", out[1],
+          "frac %.4f" % (out[1] / max(out[0], 1)), "undecided evaluations", out[2],
+          "per evaluation %.6f" % (out[2] / max(out[0] * 64, 1)))
