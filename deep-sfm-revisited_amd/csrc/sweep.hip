@@ -256,6 +256,286 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep(const float* __restrict__ 
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Cost volume, aligned-slab form (default, tuning key sweep_flat = 1).
+//
+// Each output row (b, r) of the [B, rows, L, h, w] volume is one contiguous
+// slab of L*h*w elements.  A work item is a 1024-element window of the slabs
+// of one channel group: G = 4*NQ warped rows (channels 4*NQ*k ..) and, for
+// the full volume, the G reference rows of the same channels.  Window starts
+// are 256-byte aligned in absolute address (a window may straddle two
+// planes), so every wave store is one aligned 256-byte segment.
+//   * scripts/probe_store_bw2.hip (profiles/r01_probe_store_bw2.txt): stores
+//     of this shape run at 6.3-7.0 TB/s on MI355X for 1-8 rows per item, the
+//     per-row windows above at 4.0-5.0 (their 256-byte wave segments straddle
+//     cache lines: rows start at arbitrary 4-byte offsets).
+//   * Pairing the copy rows with the warped rows in one item keeps every
+//     block half store-bound, half VALU-bound, so the two overlap on every
+//     CU instead of alternating between all-copy and all-warp phases.
+//   * One item per block, items in address order (window fastest): the
+//     resident blocks sweep a narrow front of the 2G slabs.
+//   * Every vector-memory byte passes the CU's 64 B/clk L1 path: per 4-byte
+//     output ~8 B of tap gathers (16 B per warped output), 2 B of reference
+//     loads and the 4 B store.  Rays K^-1 (x, y, 1) are therefore recomputed
+//     (18 VALU) rather than read from a per-pixel table (16 B per pixel and
+//     plane; measured 1.36 vs 1.32 ms at KITTI B=8, L=128).
+// Arithmetic: the reference's float32 expression order (warp.h
+// sample_pos_nr: the same bits as sample_pos with Newton-Raphson divisions),
+// the bilinear taps in the in-image form (make_taps_inside), and FMA in the
+// 4-tap sum (within 1 ulp of the per-row kernel's mul/add chain).  Uniform
+// integer divisions use magic numbers.
+// ---------------------------------------------------------------------------
+constexpr int kFlatWin = 1024;
+
+struct Magic {   // floor(n / d) = (n * m) >> s for 0 <= n < 2^31
+  unsigned m, s;
+};
+static Magic make_magic(unsigned d) {
+  unsigned l = 0;
+  while ((1ull << l) < d) ++l;
+  const unsigned long long two = 1ull << (31 + l);
+  return Magic{(unsigned)((two + d - 1) / d), 31 + l};
+}
+__device__ __forceinline__ unsigned magic_div(unsigned n, Magic mg) {
+  return (unsigned)(((unsigned long long)n * mg.m) >> mg.s);
+}
+
+struct FlatGeom {
+  int B, C, C4, h, w, L, hw;
+  int ref_rows, rows;
+  int G;           // channels per group (4 * NQ)
+  int groups;      // ceil(C / G) per pair
+  int slab;        // L * hw elements
+  int nwin;        // windows per slab
+  int amask;       // elements per 256 bytes - 1
+  int out_mis;     // element offset of the output pointer modulo amask + 1
+  int pair_ok;     // bf16: every row starts at an even element (4-byte pair stores)
+  Magic mwin, mgrp, mhw;
+  float inv_w;
+  float dmax, dstep;
+};
+
+template <typename OutT> struct FlatLanes;   // pixels per lane per store, stores per lane per row
+template <> struct FlatLanes<float> { static constexpr int PXL = 1, NS = 4; };
+template <> struct FlatLanes<unsigned short> { static constexpr int PXL = 2, NS = 2; };
+
+__device__ __forceinline__ float plane_depth(float dmax, float dstep, int l) {
+  // PSNet.py:150-153: depth planes (i+1)*MIN_DEPTH, or disp2depth / (i+1)
+  return dstep > 0.0f ? (float)(l + 1) * dstep : dmax / (float)(l + 1);
+}
+
+template <typename OutT, int PXL>
+__device__ __forceinline__ void store_px(OutT* row, int f0, int slab, bool pair_ok, const float* v) {
+  if (PXL == 1) {
+    if (f0 >= 0 && f0 < slab) store1(row + f0, v[0]);
+  } else {
+    if (pair_ok && f0 >= 0 && f0 + 1 < slab) {
+      const unsigned int u = (unsigned int)to_bf16(v[0]) | ((unsigned int)to_bf16(v[1]) << 16);
+      *reinterpret_cast<unsigned int*>(row + f0) = u;
+    } else {
+#pragma unroll
+      for (int k = 0; k < PXL; ++k)
+        if (f0 + k >= 0 && f0 + k < slab) store1(row + f0 + k, v[k]);
+    }
+  }
+}
+
+// Bilinear taps of an in-image sample (sample_pos returned true): then
+// ix in [0, w-1] and iy in [0, h-1] exactly (monotone rounding of
+// ((xn + 1) / 2) (w - 1) with |xn| <= 1), so x0, y0 are valid and x1 = w
+// (y1 = h) only when ix = w - 1 exactly, where its weight ix - x0 is +0: the
+// taps and weights equal make_taps' (invalid taps there weigh 0), without
+// the validity tests.  Addresses of such taps are clamped.
+struct TapsIn {
+  unsigned off[4];
+  float wt[4];
+};
+__device__ __forceinline__ void make_taps_inside(float ix, float iy, int h, int w, TapsIn& t) {
+  const float fx = floorf(ix), fy = floorf(iy);
+  const int x0 = (int)fx, y0 = (int)fy;
+  const float wx1 = ix - fx, wx0 = (fx + 1.0f) - ix;
+  const float wy1 = iy - fy, wy0 = (fy + 1.0f) - iy;
+  t.wt[0] = wx0 * wy0;
+  t.wt[1] = wx1 * wy0;
+  t.wt[2] = wx0 * wy1;
+  t.wt[3] = wx1 * wy1;
+  const unsigned o0 = (unsigned)__mul24(y0, w) + (unsigned)x0;
+  const unsigned dx = x0 < w - 1 ? 1u : 0u, dy = y0 < h - 1 ? (unsigned)w : 0u;
+  t.off[0] = o0;
+  t.off[1] = o0 + dx;
+  t.off[2] = o0 + dy;
+  t.off[3] = o0 + dy + dx;
+}
+
+// base + a 32-bit byte offset: uniform base pointers stay in SGPRs and the
+// accesses use the saddr + 32-bit voffset form (no 64-bit address VALU).
+template <typename T>
+__device__ __forceinline__ T* at_u32(T* base, unsigned byte_off) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off);
+}
+template <typename T>
+__device__ __forceinline__ const T* at_u32(const T* base, unsigned byte_off) {
+  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
+// One item's body.  INTERIOR: the window lies inside the slab (every lane
+// pixel valid; unguarded stores), else edge windows with per-pixel guards.
+template <typename OutT, int NQ, bool INTERIOR>
+__device__ __forceinline__ void sweep_flat_item(const float* __restrict__ ref, const f32x4* __restrict__ tq,
+                                                const float* __restrict__ pose,
+                                                const float* __restrict__ K4, const float* __restrict__ K4inv,
+                                                const FlatGeom& g, OutT* __restrict__ out, int b, int k,
+                                                int start, size_t wbase) {
+  constexpr int PXL = FlatLanes<OutT>::PXL, NS = FlatLanes<OutT>::NS, NPX = PXL * NS;
+  constexpr int G = 4 * NQ;
+  const int c0 = k * G;
+  const int l0 = (int)magic_div((unsigned)max(start, 0), g.mhw);
+  const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+  // lane pixels: slab index f = start + 256 wave + 64 PXL s + PXL lane + e
+  int fs[NS], ps[NPX], ls[NPX];
+  const int pbase = start - l0 * g.hw;         // in-plane index of the window start (< 0 only at an edge)
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    fs[s] = start + 256 * wave + 64 * PXL * s + PXL * lane;
+#pragma unroll
+    for (int e = 0; e < PXL; ++e) {
+      int p = pbase + 256 * wave + 64 * PXL * s + PXL * lane + e, l = l0;
+      if (!INTERIOR) {
+        const int f = fs[s] + e;
+        if (f < 0 || f >= g.slab) p = 0;
+      }
+      while (p >= g.hw) { p -= g.hw; ++l; }
+      ps[s * PXL + e] = p;
+      ls[s * PXL + e] = l;
+    }
+  }
+  const int nc = min(G, g.C - c0);
+  // reference rows of the group: loads first (in flight during the warp)
+  float cp[G][NPX];
+  if (g.ref_rows) {
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      if (c >= nc) break;
+      const float* R = ref + ((size_t)b * g.C + c0 + c) * g.hw;
+#pragma unroll
+      for (int j = 0; j < NPX; ++j) cp[c][j] = *at_u32(R, (unsigned)ps[j] * 4u);
+    }
+  }
+  Proj pr;
+  load_proj(pose, K4, K4inv, b, pr);
+  const SampleK sk = sample_consts(g.h, g.w);
+  const float dA = plane_depth(g.dmax, g.dstep, l0), dB = plane_depth(g.dmax, g.dstep, l0 + 1);
+  const f32x4* Tb = tq + ((size_t)b * g.C4 + k * NQ) * g.hw;
+  f32x4 acc[NQ][NPX];
+#pragma unroll
+  for (int j = 0; j < NPX; ++j) {
+    const int p = ps[j], l = ls[j];
+    float d = l == l0 ? dA : dB;
+    if (l > l0 + 1) d = plane_depth(g.dmax, g.dstep, l);   // feature maps under 1024 pixels
+    // pixel (x, y) = (p % w, p / w): float reciprocal and one correction (p < 2^24),
+    // then the ray K^-1 (x, y, 1) in the reference's order (pixel2cam)
+    int y = (int)((float)p * g.inv_w);
+    int x = p - y * g.w;
+    if (x < 0) { --y; x += g.w; }
+    if (x >= g.w) { ++y; x -= g.w; }
+    const float xf = (float)x, yf = (float)y;
+    float ray[3];
+    ray[0] = (pr.ki[0] * xf + pr.ki[1] * yf) + pr.ki[2];
+    ray[1] = (pr.ki[3] * xf + pr.ki[4] * yf) + pr.ki[5];
+    ray[2] = (pr.ki[6] * xf + pr.ki[7] * yf) + pr.ki[8];
+    float ix, iy;
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) acc[n][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (sample_pos_nr(pr, ray, d, sk, ix, iy)) {
+      TapsIn tp;
+      make_taps_inside(ix, iy, g.h, g.w, tp);
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        if (4 * n >= nc) break;
+        const f32x4* T = Tb + (size_t)n * g.hw;
+        const f32x4 t0 = *at_u32(T, tp.off[0] * 16u), t1 = *at_u32(T, tp.off[1] * 16u);
+        const f32x4 t2 = *at_u32(T, tp.off[2] * 16u), t3 = *at_u32(T, tp.off[3] * 16u);
+        f32x4 a;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = tp.wt[0] * t0[e];
+          v = __builtin_fmaf(tp.wt[1], t1[e], v);
+          v = __builtin_fmaf(tp.wt[2], t2[e], v);
+          a[e] = __builtin_fmaf(tp.wt[3], t3[e], v);
+        }
+        acc[n][j] = a;
+      }
+    }
+  }
+  // stores: row base + 32-bit byte offset of the window (slab < 2^30 elements)
+  auto store_row = [&](OutT* row, const float* v) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (INTERIOR) {
+        OutT* dst = at_u32(row, (unsigned)fs[s] * (unsigned)sizeof(OutT));
+        if (PXL == 1) {
+          store1(dst, v[s]);
+        } else {
+          const unsigned int u = (unsigned int)to_bf16(v[2 * s]) | ((unsigned int)to_bf16(v[2 * s + 1]) << 16);
+          if (g.pair_ok) *reinterpret_cast<unsigned int*>(dst) = u;
+          else { store1(dst, v[2 * s]); store1(dst + 1, v[2 * s + 1]); }
+        }
+      } else {
+        store_px<OutT, PXL>(row, fs[s], g.slab, g.pair_ok, v + s * PXL);
+      }
+    }
+  };
+  if (g.ref_rows) {
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      if (c >= nc) break;
+      store_row(out + ((size_t)b * g.rows + c0 + c) * (size_t)g.slab, cp[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < G; ++c) {
+    if (c >= nc) break;
+    float v[NPX];
+#pragma unroll
+    for (int j = 0; j < NPX; ++j) v[j] = acc[c >> 2][j][c & 3];
+    store_row(out + wbase + (size_t)c * g.slab, v);
+  }
+}
+
+template <typename OutT, int NQ>
+__global__ __launch_bounds__(kSwThreads) void k_sweep_flat(const float* __restrict__ ref,
+                                                           const f32x4* __restrict__ tq,
+                                                           const float* __restrict__ pose,
+                                                           const float* __restrict__ K4,
+                                                           const float* __restrict__ K4inv, FlatGeom g,
+                                                           OutT* __restrict__ out) {
+  const unsigned item = blockIdx.x;            // grid = B * groups * nwin
+  const unsigned r = magic_div(item, g.mwin);
+  const int win = (int)(item - r * (unsigned)g.nwin);
+  const int b = (int)magic_div(r, g.mgrp);
+  const int k = (int)(r - (unsigned)b * (unsigned)g.groups);
+  const size_t wbase = ((size_t)b * g.rows + g.ref_rows + k * 4 * NQ) * (size_t)g.slab;   // first warped row
+  const int start = win * kFlatWin - (int)((wbase + (size_t)g.out_mis) & (size_t)g.amask);
+  if (start >= g.slab) return;
+  if (start >= 0 && start + kFlatWin <= g.slab)
+    sweep_flat_item<OutT, NQ, true>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
+  else
+    sweep_flat_item<OutT, NQ, false>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
+}
+
+template <typename OutT>
+static void launch_k_sweep_flat(int nq, unsigned blocks, hipStream_t s, const float* ref, const f32x4* tq,
+                                const float* pose, const float* K4, const float* K4inv, const FlatGeom& g,
+                                void* out) {
+  if (nq == 2)
+    hipLaunchKernelGGL((k_sweep_flat<OutT, 2>), dim3(blocks), dim3(kSwThreads), 0, s, ref, tq, pose, K4, K4inv, g,
+                       (OutT*)out);
+  else
+    hipLaunchKernelGGL((k_sweep_flat<OutT, 1>), dim3(blocks), dim3(kSwThreads), 0, s, ref, tq, pose, K4, K4inv, g,
+                       (OutT*)out);
+}
+
 // inverse_warp for an arbitrary depth map (models/inverse_warp.py:121-153)
 __global__ __launch_bounds__(kSweepThreads) void k_inverse_warp(const float* __restrict__ feat, int C, int h, int w,
                                                                 const float* __restrict__ depth,
@@ -316,6 +596,7 @@ static void launch_k_sweep(int ipb, int64_t blocks, hipStream_t s, const float* 
   else launch_k_sweep_lp<OutT, VEC, false, false>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
 }
 
+// workspace: channel quads tq [B][C4][hw] float4
 static size_t sweep_ws_bytes(int B, int C, int h, int w) {
   const int C4 = (C + 3) / 4;
   return (size_t)B * C4 * (size_t)h * w * sizeof(f32x4);
@@ -359,7 +640,34 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     launch_channel_quads(tgt, B, C, hw, tq, s);
   }
   SFM_LAUNCHED();
-  ProfScope ps(with_ref ? "plane_sweep" : "plane_sweep_warped", s);
+  const char* pname = with_ref ? "plane_sweep" : "plane_sweep_warped";
+  // aligned-slab form: int slab offsets, 31-bit magic-number decode
+  const int nq = tuning().sweep_group == 8 ? 2 : 1;
+  const int64_t slab = (int64_t)L * hw;
+  const int fgroups = (C + 4 * nq - 1) / (4 * nq);
+  const int64_t nwin = (slab + 127 + kFlatWin - 1) / kFlatWin;
+  if (tuning().sweep_flat && hw < (1 << 24) && slab < ((int64_t)1 << 30) && (int64_t)B * fgroups * nwin < ((int64_t)1 << 31)) {
+    FlatGeom fg;
+    fg.B = B; fg.C = C; fg.C4 = g.C4; fg.h = h; fg.w = w; fg.L = L; fg.hw = hw;
+    fg.ref_rows = g.ref_rows; fg.rows = g.rows; fg.G = 4 * nq; fg.groups = fgroups;
+    fg.slab = (int)slab; fg.nwin = (int)nwin;
+    const int esz = out_dtype == 0 ? 4 : 2;
+    fg.amask = 256 / esz - 1;
+    fg.out_mis = (int)(((uintptr_t)out / esz) & (uintptr_t)fg.amask);
+    fg.pair_ok = (slab % 2 == 0) && ((uintptr_t)out % 4 == 0);
+    fg.mwin = make_magic((unsigned)nwin);
+    fg.mgrp = make_magic((unsigned)fgroups);
+    fg.mhw = make_magic((unsigned)hw);
+    fg.inv_w = 1.0f / (float)w;
+    fg.dmax = g.dmax; fg.dstep = g.dstep;
+    const unsigned blocks = (unsigned)((int64_t)B * fgroups * nwin);
+    ProfScope ps(pname, s);
+    if (out_dtype == 0) launch_k_sweep_flat<float>(nq, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+    else launch_k_sweep_flat<unsigned short>(nq, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+    SFM_LAUNCHED();
+    return SFM_OK;
+  }
+  ProfScope ps(pname, s);
   if (out_dtype == 0) {
     if (vec) launch_k_sweep<float, true>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
     else launch_k_sweep<float, false>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);

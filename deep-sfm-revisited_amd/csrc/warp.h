@@ -53,6 +53,74 @@ __device__ __forceinline__ bool sample_pos(const Proj& pr, const float ray[3], f
   return true;
 }
 
+// IEEE float32 division a / b (the reference's '/') by the Newton-Raphson
+// steps of the compiler's V_DIV_SCALE / V_DIV_FMAS / V_DIV_FIXUP expansion,
+// without its range scaling and special-case fixup.  Bit-identical to '/'
+// whenever the expansion would not scale or fix up: a, b, 1/b and a/b normal
+// and finite, |a| >= 2^-103 and exponent(a) - exponent(b) < 96.  y = rcp_nr(b).
+__device__ __forceinline__ float rcp_nr(float b) {
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  const float e = __builtin_fmaf(-b, y0, 1.0f);
+  return __builtin_fmaf(e, y0, y0);
+}
+__device__ __forceinline__ float div_nr(float a, float b, float y) {
+  const float q0 = a * y;
+  const float r0 = __builtin_fmaf(-b, q0, a);
+  const float q1 = __builtin_fmaf(r0, y, q0);
+  const float r1 = __builtin_fmaf(-b, q1, a);
+  return __builtin_fmaf(r1, y, q1);
+}
+
+// Per-launch constants of sample_pos_nr (uniform).
+struct SampleK {
+  float cw, ch;     // (float)(w - 1), (float)(h - 1)
+  float yw, yh;     // rcp_nr of each
+  float hw1, hh1;   // (w - 1) / 2, (h - 1) / 2 (exact)
+};
+__device__ __forceinline__ SampleK sample_consts(int h, int w) {
+  SampleK k;
+  k.cw = (float)(w - 1);
+  k.ch = (float)(h - 1);
+  k.yw = rcp_nr(k.cw);
+  k.yh = rcp_nr(k.ch);
+  k.hw1 = 0.5f * k.cw;
+  k.hh1 = 0.5f * k.ch;
+  return k;
+}
+
+// sample_pos with its four divisions in the Newton-Raphson form: the same
+// decision and the same ix, iy bits.
+//  * X / Z and Y / Z: |X|, |Y| <= 2^60 and 1e-3 <= Z <= 2^60 keep div_nr in
+//    its exact range, except for |X| < 2^-103 (or a denormal quotient), where
+//    the quotient may differ in its last bits but 2 q / (w - 1) - 1 rounds to
+//    exactly -1 either way.  Other operands (huge or NaN) take '/'.
+//  * 2 q / (w - 1): |2 q| <= 2^71 against w - 1 >= 1; tiny 2 q as above.
+//  * ((xn + 1) / 2) (w - 1) = (xn + 1) ((w - 1) / 2): the halving is exact,
+//    so both are the one rounding of the same real product.
+__device__ __forceinline__ bool sample_pos_nr(const Proj& pr, const float ray[3], float d, const SampleK& k,
+                                              float& ix, float& iy) {
+  const float c0 = ray[0] * d, c1 = ray[1] * d, c2 = ray[2] * d;
+  const float X = ((pr.m[0] * c0 + pr.m[1] * c1) + pr.m[2] * c2) + pr.m[3];
+  const float Y = ((pr.m[4] * c0 + pr.m[5] * c1) + pr.m[6] * c2) + pr.m[7];
+  float Z = ((pr.m[8] * c0 + pr.m[9] * c1) + pr.m[10] * c2) + pr.m[11];
+  Z = Z < 1e-3f ? 1e-3f : Z;
+  float qx, qy;
+  if (fabsf(X) <= 0x1p60f && fabsf(Y) <= 0x1p60f && Z <= 0x1p60f) {
+    const float yz = rcp_nr(Z);
+    qx = div_nr(X, Z, yz);
+    qy = div_nr(Y, Z, yz);
+  } else {
+    qx = X / Z;
+    qy = Y / Z;
+  }
+  const float xn = div_nr(2.0f * qx, k.cw, k.yw) - 1.0f;
+  const float yn = div_nr(2.0f * qy, k.ch, k.yh) - 1.0f;
+  if (!(xn <= 1.0f && xn >= -1.0f && yn <= 1.0f && yn >= -1.0f)) return false;
+  ix = (xn + 1.0f) * k.hw1;
+  iy = (yn + 1.0f) * k.hh1;
+  return true;
+}
+
 struct Taps {
   int off[4];
   float wt[4];

@@ -39,7 +39,7 @@ for rnd in range(3):
         _lib.tune("solve_lanes", 32)
     for lp in (0, 1, 2):
         _lib.tune("sweep_lane_pixels", lp)
-        for ipb in (2, 4, 8):
+        for ipb in (1, 2, 4, 8):
             _lib.tune("sweep_items_per_block", ipb)
             res.setdefault(f"sweep_lp={lp}_ipb={ipb}", []).append(timed("plane_sweep", lambda: hp.sweep(ref, tgt, P0, K)))
             assert torch.equal(hp.cost, c0), "results changed with sweep knobs"

@@ -1,0 +1,56 @@
+"""The aligned-slab sweep kernel (k_sweep_flat, the default) against the
+per-row kernel (tuning key sweep_flat=0) and the oracle: both group sizes,
+edge windows, feature maps under one 1024-pixel window, odd slabs and output
+pointers off the 256-byte grid.  Sample positions are bit-identical
+(warp.h sample_pos_nr); the 4-tap sum differs by FMA rounding only."""
+import pytest
+import torch
+
+from oracle import sweep as S
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 1e-4, 1e-4
+
+
+@pytest.mark.parametrize("B,C,L,h,w,dtype,offset", [
+    (2, 32, 16, 47, 156, torch.float32, 0),    # slab % 64 != 0: per-row misaligned groups
+    (1, 6, 5, 13, 21, torch.float32, 1),       # hw < 1024: windows span several planes; out 4 B off
+    (1, 10, 4, 20, 64, torch.float32, 3),      # slab % 64 == 0, output pointer misaligned
+    (1, 5, 3, 11, 19, torch.bfloat16, 1),      # odd slab: bf16 element stores
+    (2, 12, 6, 16, 40, torch.bfloat16, 0),     # bf16 pair stores, partial group of 8
+])
+def test_aligned_slab_kernel_matches_per_row(cuda, B, C, L, h, w, dtype, offset):
+    from sfm_amd import _lib, synth
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
+    ref, tgt = synth.features(B, C, h, w, seed=C * L + w)
+    K = synth.intrinsics(B, 4.0 * w, 4.0 * w, 2.0 * w, 2.0 * h)
+    Ki = torch.inverse(K)
+    pose = synth.relative_pose(B, torch.Generator().manual_seed(L + h))
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    args = (ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 0.8)
+    n = B * 2 * C * L * h * w
+    outs = {}
+    try:
+        for flat, group in ((0, 4), (1, 4), (1, 8)):
+            _lib.tune("sweep_flat", flat)
+            _lib.tune("sweep_group", group)
+            buf = torch.full((n + offset,), float("nan"), dtype=dtype, device=cuda)
+            out = buf[offset:].view(B, 2 * C, L, h, w)
+            plane_sweep_cost(*args, dtype=dtype, out=out)
+            outs[(flat, group)] = out.float().cpu()
+    finally:
+        _lib.tune("sweep_flat", 1)
+        _lib.tune("sweep_group", 8)
+    base = outs[(0, 4)]
+    assert not torch.isnan(base).any()
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    for key in ((1, 4), (1, 8)):
+        got = outs[key]
+        assert not torch.isnan(got).any(), key            # every element written
+        assert torch.equal(got[:, :C], base[:, :C]), key  # reference half: exact copy
+        assert float((got - base).abs().max()) <= tol, (key, float((got - base).abs().max()))
+    if dtype == torch.float32:
+        want = S.plane_sweep_cost(ref, tgt, pose, K, Ki, L, 0.8)
+        err = (outs[(1, 4)] - want).abs() - (RTOL * want.abs() + ATOL)
+        assert float(err.max()) <= 0.0, float((outs[(1, 4)] - want).abs().max())
