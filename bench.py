@@ -144,8 +144,10 @@ def main():
     if hp.fused:
         kt.pop("flow_to_points", None)
     evals = sum(cands) * hp.n                       # candidate E x correspondences per launch
+    skipped = ransac.skipped_evaluations(hp.ws, B, args.iters)   # exact bound pruning (last launch)
+    done = evals - skipped                          # evaluations the launch performed
     score_ms = kt["ransac_score"]
-    score_tflops = evals * FLOP_PER_EVAL / (score_ms * 1e-3) / 1e12
+    score_tflops = done * FLOP_PER_EVAL / (score_ms * 1e-3) / 1e12
     h, w = fhw
     s = 4 if cost_dtype == torch.float32 else 2
     sweep_bytes = B * (2 * C * args.nlabel * h * w * s + 2 * C * h * w * 4)
@@ -177,7 +179,9 @@ def main():
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(score_tflops / PEAK_FP32_TFLOPS, 4),
                          "traffic": traffic.get("ransac_score"), "traffic_source": traffic_src,
                          "avg_launch_ms": round(score_ms, 4),
-                         "work": f"{evals} evals x {FLOP_PER_EVAL} FLOP per launch ({sum(cands)} candidate E)"},
+                         "work": (f"{done} evals x {FLOP_PER_EVAL} FLOP per launch: {sum(cands)} candidate E x "
+                                  f"N={hp.n} = {evals}, minus {skipped} skipped by exact bound pruning "
+                                  f"({100.0 * skipped / max(evals, 1):.1f}%)")},
             "roofline_sweep": {"kernel": "plane_sweep", "bound": "hbm", "achieved": round(sweep_gbs, 1),
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(sweep_gbs / PEAK_HBM_GBS, 4),
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,

@@ -19,6 +19,8 @@ struct Tuning {
   int sweep_group = 8;           // warped channels per k_sweep_flat item (4 or 8; 8 measured stable in the bench loop)
   int score_blocks_per_cu = 32;  // persistent score grid
   int score_fp32 = 1;            // packed float32 pre-decision in the score kernel
+  int score_prune = 1;           // exact bound pruning in k_score32 (PruneState)
+  int score_interleave = 0;      // k_score32 items: pairs interleaved (1) or pair after pair (0)
 };
 Tuning& tuning();
 

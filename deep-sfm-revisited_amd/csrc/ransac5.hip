@@ -64,10 +64,13 @@ struct Workspace {
   int32_t* cntT;       // [B][Cmax]
   int32_t* cntR;       // [B][Cmax]
   int32_t* score;      // [B][H]
+  unsigned long long* cov;      // [B][Cmax] pruning bound state: count | points covered << 32
+  int32_t* best_lb;             // [64] largest partial count seen (a lower bound on the winning score)
+  unsigned long long* skipped;  // [1] evaluations skipped by pruning (whole call)
   double* pack;        // [n_max][4]
 };
 
-static inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+__host__ __device__ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
 // Lay out the workspace; returns the byte count (ptrs filled when base != nullptr).
 static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w) {
@@ -86,6 +89,9 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   t.candE = (double*)take(bc * C * kCandStride * 8);
   t.cntT = (int32_t*)take(bc * C * 4);
   t.cntR = (int32_t*)take(bc * C * 4);
+  t.cov = (unsigned long long*)take(bc * C * 8);     // must follow cntR (prune_state)
+  t.best_lb = (int32_t*)take(SFM_MAX_BATCH * 64 * 4);    // kBestStride
+  t.skipped = (unsigned long long*)take(8);
   t.score = (int32_t*)take(bc * H * 4);
   t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
   if (w) *w = t;
@@ -448,7 +454,51 @@ struct ScoreConsts {
   double thr, t2lo, t2hi;
   float t2lo32, t2hi32;
   int fast32;
+  int prune;      // exact bound pruning on (PruneState)
+  int interleave; // k_score32 item order: pairs interleaved (1) or one after another (0)
+  int ws_batch;   // pairs the workspace was laid out for (locates PruneState)
 };
+
+// Exact bound pruning in k_score32 (tuning key score_prune; only when
+// num_test == num_ransac_test, SFMnet's case, and no per-hypothesis scores
+// are requested).  A candidate's final count is at most its count so far plus
+// the points not yet scored for it.  Once that bound is below the largest
+// count any candidate of the pair has reached so far, the candidate can be
+// neither the winner nor decide it, so its remaining spans are skipped:
+//   * best_lb only ever holds partial counts, each <= its candidate's final
+//     count <= the winning score.
+//   * a pruned candidate's true count is < best_lb.  If it loses its
+//     hypothesis's preselection because its partial count is lower, that
+//     hypothesis's true best is < best_lb too, so it cannot win.  Any
+//     hypothesis or chain reaching the winning score has only unpruned, exact
+//     counts (ties included).
+//   * cov packs (count, points covered) in one 64-bit atomic, so every read
+//     is a consistent snapshot.  Updates only lower count + (T - covered), and
+//     only raise best_lb, so stale reads only prune less.
+// The winner, its count, E and P are therefore identical with pruning on or
+// off.  The per-hypothesis scores of losing hypotheses are lower bounds.
+constexpr uint32_t kPrunedFlag = 0xBF800000u;   // record slot 10+13 (ok32) of a pruned candidate: -1.0f
+constexpr int kBestStride = 64;                  // best_lb[b * kBestStride]: one 256-byte line per pair
+
+// The pruning state follows cntR in the workspace (layout): cov [B][cmax]
+// (count | points covered << 32), best_lb [64], skipped.  The score kernel
+// derives it from cntR where it is used: its SGPRs are at the limit, and
+// three more live pointers spill the hot loop.
+struct PruneState {
+  unsigned long long* cov;
+  int32_t* best_lb;
+  unsigned long long* skipped;
+};
+__host__ __device__ inline PruneState prune_state(int32_t* cntR, int ws_batch, int cmax) {
+  char* p = reinterpret_cast<char*>(cntR) + align_up((size_t)ws_batch * cmax * 4);
+  PruneState st;
+  st.cov = reinterpret_cast<unsigned long long*>(p);
+  p += align_up((size_t)ws_batch * cmax * 8);
+  st.best_lb = reinterpret_cast<int32_t*>(p);
+  p += align_up((size_t)SFM_MAX_BATCH * kBestStride * 4);
+  st.skipped = reinterpret_cast<unsigned long long*>(p);
+  return st;
+}
 
 // Exact reference evaluation (ComputeError, kernel_functions.cu:232-264).
 __device__ __forceinline__ bool inlier_exact(double a, double D, double thr) {
@@ -718,7 +768,9 @@ __device__ __forceinline__ int score32_pass(const double* __restrict__ CE, int c
     const float* F = reinterpret_cast<const float*>(CE + (size_t)c * kCandStride + 10);
     int sT = 0, sR = 0;
     uint64_t undk[kPPL32];
-    if (__builtin_amdgcn_readfirstlane(__float_as_uint(F[13])) != 0u) {   // ok32 (wave-uniform: 1.0f or 0.0f)
+    const uint32_t ok32 = __builtin_amdgcn_readfirstlane(__float_as_uint(F[13]));   // 1.0f, 0.0f or pruned
+    if (ok32 == kPrunedFlag) continue;                  // exact bound pruning (PruneState)
+    if (ok32 != 0u) {
       const float e0 = F[0], e1 = F[1], e2 = F[2], e3 = F[3], e4 = F[4], e5 = F[5], e6 = F[6], e7 = F[7], e8 = F[8];
       float neps1, eps2;
       if (GEN) {
@@ -840,21 +892,25 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
                ScoreConsts kc) {
   constexpr int kWaves = kScoreThreads / 64;
   __shared__ int32_t s_cnt[kWaves][kKC][2];
-  __shared__ int32_t s_items[SFM_MAX_BATCH + 1];
+  __shared__ int32_t s_items[SFM_MAX_BATCH + 1];   // items per pair; [batch] = total
+  __shared__ int32_t s_first[SFM_MAX_BATCH + 1];   // pair-major order: first item of each pair
   __shared__ int32_t s_tiles[SFM_MAX_BATCH];
   __shared__ double2 s_cand[kWaves][kKC * kCandStride / 2];
   __shared__ uint32_t s_queue[kWaves][kQueue];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) {
-    int acc = 0;
+    int most = 0, acc = 0;
     for (int b = 0; b < batch; ++b) {
       const int tiles = (cand_total[b] + kKC - 1) / kKC;
       const int splits = (max(pp.test[b], pp.rtest[b]) + kPtsPerWave - 1) / kPtsPerWave;
       s_tiles[b] = tiles;
-      s_items[b] = acc;
+      s_items[b] = tiles * splits;
+      s_first[b] = acc;
       acc += tiles * splits;
+      most = max(most, tiles * splits);
     }
-    s_items[batch] = acc;
+    s_first[batch] = acc;
+    s_items[batch] = kc.interleave ? most * batch : acc;
   }
   for (int i = tid; i < kWaves * kKC * 2; i += kScoreThreads) (&s_cnt[0][0][0])[i] = 0;
   __syncthreads();
@@ -863,12 +919,23 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
   const double* CE = reinterpret_cast<const double*>(s_cand[wv]);
   const int total = __builtin_amdgcn_readfirstlane(s_items[batch]);
   const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
+  // Items run split-major within a pair (every candidate of a pair advances
+  // through its points together), pairs one after another, or interleaved
+  // (item % batch, tuning key score_interleave).
+  unsigned long long skipped = 0;                               // evaluations pruned by this wave
   for (int item = gw; item < total; item += gridDim.x * kWaves) {
-    int b = 0;
-    while (item >= s_items[b + 1]) ++b;
-    b = __builtin_amdgcn_readfirstlane(b);                      // wave-uniform (LDS-derived)
+    int b, local;
+    if (kc.interleave) {
+      b = __builtin_amdgcn_readfirstlane(item % batch);
+      local = item / batch;
+      if (local >= __builtin_amdgcn_readfirstlane(s_items[b])) continue;   // ragged batch: this pair is done
+    } else {
+      b = 0;
+      while (item >= s_first[b + 1]) ++b;
+      b = __builtin_amdgcn_readfirstlane(b);                    // wave-uniform (LDS-derived)
+      local = item - __builtin_amdgcn_readfirstlane(s_first[b]);
+    }
     const int tiles = __builtin_amdgcn_readfirstlane(s_tiles[b]);
-    const int local = item - __builtin_amdgcn_readfirstlane(s_items[b]);
     const int split = local / tiles, tile = local - split * tiles;
     const int ctot = cand_total[b];
     const int c0 = tile * kKC;
@@ -883,8 +950,25 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
       for (int i = lane; i < nc * (kCandStride / 2); i += 64) s_cand[wv][i] = srcc[i];
     }
     wave_sync();
+    // candidates whose bound count + (T - covered) is below the pair's best
+    // count so far: flagged in this wave's LDS record (score32_pass skips them)
+    bool all_pruned = false;
+    int lb = 0;
+    if (kc.prune) {
+      const PruneState st = prune_state(cntR, kc.ws_batch, cmax);
+      lb = __hip_atomic_load(st.best_lb + (size_t)b * kBestStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bool pr = false;
+      if (lane < nc) {
+        const unsigned long long v = __hip_atomic_load(st.cov + (size_t)b * cmax + c0 + lane, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        pr = (long long)(uint32_t)v + (long long)T - (long long)(v >> 32) < (long long)lb;
+        if (pr) reinterpret_cast<float*>(s_cand[wv])[(lane * kCandStride + 10) * 2 + 13] = __uint_as_float(kPrunedFlag);
+      }
+      all_pruned = __ballot(pr) == lane_prefix(nc);
+      wave_sync();
+    }
     int qn = 0;
-    for (int cb = p0; cb < p1; cb += 64 * kPPL32) {
+    for (int cb = all_pruned ? p1 : p0; cb < p1; cb += 64 * kPPL32) {
       int c = 0;
       for (;;) {
         // (re)load the chunk: the points are dead while the queue drains
@@ -927,6 +1011,31 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
     score32_drain(CE, src, b, T, R, kc, lane, cnt, queue, qn);
 #endif
     wave_sync();
+    if (kc.prune) {
+      // publish (count, covered) of the span; raise the pair's best count so far
+      const PruneState st = prune_state(cntR, kc.ws_batch, cmax);
+      int reached = 0, skip = 0;
+      if (lane < nc) {
+        const float* F = reinterpret_cast<const float*>(CE + (size_t)lane * kCandStride + 10);
+        if (__float_as_uint(F[13]) == kPrunedFlag) {
+          skip = p1 - p0;
+        } else {
+          const int sc = cnt[lane][0];
+          const unsigned long long old = atomicAdd(st.cov + (size_t)b * cmax + c0 + lane,
+                                                   ((unsigned long long)(p1 - p0) << 32) | (unsigned)sc);
+          reached = (int)(uint32_t)old + sc;
+        }
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        reached = max(reached, __shfl_xor(reached, d, 64));
+        skip += __shfl_xor(skip, d, 64);
+      }
+      // only raise the shared bound when this item beat the value it read:
+      // one hot line per pair, updated by few items
+      if (lane == 0 && reached > lb) atomicMax(st.best_lb + (size_t)b * kBestStride, reached);
+      skipped += (unsigned long long)skip;
+    }
     {
       const int c = lane >> 1, which = lane & 1;
       if (c < nc) {
@@ -937,6 +1046,7 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
     }
     wave_sync();
   }
+  if (kc.prune && lane == 0 && skipped) atomicAdd(prune_state(cntR, kc.ws_batch, cmax).skipped, skipped);
 }
 
 // ---------------------------------------------------------------------------
@@ -1121,7 +1231,7 @@ __global__ void k_keypoint_points(const float* __restrict__ flow, int H, int W, 
 template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
-                     const Workspace& w, double* E_out, double* P_out, int32_t* inliers_out,
+                     const Workspace& w, int ws_batch, double* E_out, double* P_out, int32_t* inliers_out,
                      int32_t* winner_out, int32_t* score_out, hipStream_t s) {
   const int H = kChains * iters;
   const int cmax = H * kMaxSlots;
@@ -1167,6 +1277,17 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = std::max(1, cus) * tuning().score_blocks_per_cu;
+  // exact bound pruning: SFMnet's num_test == num_ransac_test, no per-hypothesis scores requested
+  bool same = true;
+  for (int b = 0; b < bc; ++b) same = same && pp.test[b] == pp.rtest[b];
+  kc.prune = (fast32 && same && !score_out && tuning().score_prune) ? 1 : 0;
+  kc.ws_batch = ws_batch;
+  kc.interleave = tuning().score_interleave;
+  SFM_REQUIRE(prune_state(w.cntR, ws_batch, cmax).skipped == w.skipped, "internal: pruning state layout");
+  if (kc.prune) {
+    SFM_HIP(hipMemsetAsync(w.cov, 0, (size_t)bc * cmax * 8, s));
+    SFM_HIP(hipMemsetAsync(w.best_lb, 0, SFM_MAX_BATCH * kBestStride * 4, s));
+  }
   {
     ProfScope ps("ransac_score", s);
     if (fast32)
@@ -1209,10 +1330,11 @@ static int run_src(const Src& src, const int64_t* n, int batch, int num_test, in
   }
   Workspace w;
   layout((char*)ws, bc, 0, iters, &w);
+  SFM_HIP(hipMemsetAsync(w.skipped, 0, 8, s));
   const int H = kChains * iters;
   for (int b0 = 0; b0 < batch; b0 += bc) {
     const int nb = std::min(bc, batch - b0);
-    if (int rc = run_chunk(src.shifted(b0), n + b0, nb, num_test, num_ransac_test, iters, thr, seed, cheir, w,
+    if (int rc = run_chunk(src.shifted(b0), n + b0, nb, num_test, num_ransac_test, iters, thr, seed, cheir, w, bc,
                            E_out + (size_t)b0 * 9, P_out ? P_out + (size_t)b0 * 12 : nullptr, inliers_out + b0,
                            winner_out ? winner_out + b0 : nullptr,
                            score_out ? score_out + (size_t)b0 * H : nullptr, s))
@@ -1326,6 +1448,17 @@ int sfm_ransac5_candidate_counts(const void* workspace, size_t workspace_bytes, 
   Workspace w;
   layout((char*)workspace, bc, 0, iters, &w);
   SFM_HIP(hipMemcpy(counts_host, w.cand_total, sizeof(int32_t) * batch, hipMemcpyDeviceToHost));
+  return SFM_OK;
+}
+
+int sfm_ransac5_skipped_evaluations(const void* workspace, size_t workspace_bytes, int batch, int iters,
+                                    unsigned long long* skipped_host) {
+  SFM_REQUIRE(workspace && skipped_host && batch >= 1 && iters >= 1, "invalid arguments");
+  const int bc = std::min(batch, SFM_MAX_BATCH);
+  SFM_REQUIRE(workspace_bytes >= layout(nullptr, bc, 0, iters, nullptr), "workspace too small");
+  Workspace w;
+  layout((char*)workspace, bc, 0, iters, &w);
+  SFM_HIP(hipMemcpy(skipped_host, w.skipped, sizeof(unsigned long long), hipMemcpyDeviceToHost));
   return SFM_OK;
 }
 

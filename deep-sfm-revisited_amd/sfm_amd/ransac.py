@@ -152,6 +152,17 @@ def candidate_counts(workspace, batch, iters):
     return [int(v) for v in out]
 
 
+def skipped_evaluations(workspace, batch, iters):
+    """Evaluations the last RANSAC call that used ``workspace`` skipped by exact
+    bound pruning (0 when it was off; synchronises)."""
+    import ctypes
+    out = ctypes.c_uint64(0)
+    _lib.check(_lib.load().sfm_ransac5_skipped_evaluations(_lib.ptr(workspace), workspace.numel(), int(batch),
+                                                           int(iters), ctypes.byref(out)),
+               "sfm_ransac5_skipped_evaluations")
+    return int(out.value)
+
+
 KEYPOINT_MODES = {"round": 0, "sample_sp": 1, "sift_pose": 2}
 
 

@@ -150,6 +150,15 @@ int sfm_keypoints_to_points(const float* flow, int batch, int H, int W, int h_si
 int sfm_ransac5_candidate_counts(const void* workspace, size_t workspace_bytes, int batch, int iters,
                                  int32_t* counts_host);
 
+/* Evaluations the last RANSAC call with this workspace skipped by exact
+ * bound pruning (tuning key score_prune; on when num_test == num_ransac_test
+ * and hyp_score_out is NULL), copied to the host (synchronous).  The score
+ * kernel performed sum(counts) x max(num_test, num_ransac_test) minus this
+ * many evaluations.  Pruning never changes E, P, the inlier count or the
+ * winner (ransac5.hip, PruneState). */
+int sfm_ransac5_skipped_evaluations(const void* workspace, size_t workspace_bytes, int batch, int iters,
+                                    unsigned long long* skipped_host);
+
 /* Pack reference-layout q, qp (n x 2 each) into pts (n x 4). */
 int sfm_pack_points(const double* q, const double* qp, int64_t n, double* pts_out, void* stream);
 
