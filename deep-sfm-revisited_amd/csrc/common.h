@@ -20,6 +20,7 @@ struct Tuning {
   int score_blocks_per_cu = 32;  // persistent score grid
   int score_fp32 = 1;            // packed float32 pre-decision in the score kernel
   int score_prune = 1;           // exact bound pruning in k_score32 (PruneState)
+  int score_mfma = 0;            // 1: k_score_mx, linear forms on the matrix cores (measured 2.3x slower)
   int score_interleave = 0;      // k_score32 items: pairs interleaved (1) or pair after pair (0)
 };
 Tuning& tuning();

@@ -1,5 +1,5 @@
 """Score-kernel time and skipped evaluations with exact bound pruning on / off
-(KITTI B=8, H=4096, the bench workload)."""
+and the MFMA kernel on / off (KITTI B=8, H=4096, the bench workload)."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "deep-sfm-revisited_amd"))
@@ -13,9 +13,9 @@ flow, K, _, _ = synth.kitti_pair_batch(B, seed=1000, device=dev)
 hp = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 128, 8, 1e-4, 1.0, True, 0.6, device=dev)
 ref = None
 for rnd in range(2):
-    for prune, inter in ((0, 0), (1, 0), (0, 1), (1, 1)):
+    for prune, mx in ((0, 0), (1, 0), (0, 1), (1, 1)):
         _lib.tune("score_prune", prune)
-        _lib.tune("score_interleave", inter)
+        _lib.tune("score_mfma", mx)
         hp.pose(flow, K)
         torch.cuda.synchronize()
         _lib.profile_reset(); _lib.profile_enable(True)
@@ -28,6 +28,6 @@ for rnd in range(2):
         if ref is None:
             ref = out
         same = all(torch.equal(a, b) for a, b in zip(out, ref))
-        print(f"prune={prune} interleave={inter}: score {ms / n:.3f} ms, skipped {sk}, same result {same}", flush=True)
+        print(f"prune={prune} mfma={mx}: score {ms / n:.3f} ms, skipped {sk}, same result {same}", flush=True)
 _lib.tune("score_prune", 1)
-_lib.tune("score_interleave", 0)
+_lib.tune("score_mfma", 1)

@@ -81,3 +81,24 @@ def test_pruning_off_when_prefixes_differ(cuda):
     out = _both(pts, iters=2, nt=N // 2, nr=N)
     _same(out)
     assert out[1][4] == 0
+
+
+def test_mfma_scorer_is_exact(cuda):
+    """The matrix-core scorer (tuning key score_mfma, off by default) gives the
+    same per-hypothesis scores as the VALU scorer, hence the oracle's."""
+    from sfm_amd import _lib, ransac, synth
+    flow, K, _, _ = synth.kitti_pair_batch(2, seed=8, hw=(120, 200), device=cuda)
+    pts = ransac.flow_to_points(flow, torch.inverse(K))
+    outs = []
+    try:
+        for mx in (0, 1):
+            _lib.tune("score_mfma", mx)
+            outs.append(ransac.ransac5_batched(pts, iters=2, threshold=1e-4, return_scores=True))
+            torch.cuda.synchronize()
+    finally:
+        _lib.tune("score_mfma", 0)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a.cpu(), b.cpu())
+    p = pts[0].cpu().numpy()
+    ref = R.ransac5(np.ascontiguousarray(p[:, :2]), np.ascontiguousarray(p[:, 2:]), iters=2, thr=1e-4, nthreads=16)
+    assert np.array_equal(outs[1][4][0].cpu().numpy(), ref["hyp_score"])
