@@ -1,0 +1,280 @@
+// 3-D cost regularisation of PSNet on the gfx950 matrix
+// cores: the dres0..dres4 / classify stack of models/PSNet.py:79-102 applied
+// at PSNet.py:159-165, each layer a 3x3x3 / stride 1 / pad 1 Conv3d with its
+// BatchNorm3d folded into a per-channel affine (eval mode), optional ReLU and
+// optional residual add.
+//
+// Layout in HBM: activations are channels-last bf16, [B][D=nlabel][H][W][C]
+// with C = 32 (64 for the first layer's input, the [ref | warped] cost
+// volume).  Weights are packed per layer as [27 taps][32 cout][Cin] bf16
+// (cout zero-padded to 32 for the final 32 -> 1 conv).
+//
+// k_conv3: implicit GEMM, D[32 cout][pixels] = W[cout][K] . X[K][pixels],
+// K = 27 taps x Cin.  One block = 4 waves = one depth slice d, 8 output rows
+// and 64 output columns; a wave owns 4 rows x 32 columns (four 32x32
+// accumulators).  The K loop is staged through LDS one (dz, 32-channel chunk)
+// at a time: the 10 x 66 input halo of depth plane d+dz-1 and the 9 (dy, dx)
+// weight taps, 16-byte chunks XOR-swizzled so the ds_read_b128 operand reads
+// of a 16-lane group hit distinct bank slots.  The next stage is prefetched
+// into VGPRs while the current one computes.  Per stage and wave: 2 k-steps x
+// 3 dx x 12 = 72 v_mfma_f32_32x32x16_bf16 against 36 input-row and 18 weight
+// fragment reads.  The epilogue applies scale/bias, ReLU and the residual in
+// fp32 and stores bf16 four channels at a time (or, for the last layer, the
+// single output channel as fp32 [B][D][H][W], the layout the depth head reads).
+#include "common.h"
+
+namespace sfm {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kTileX = 64;          // output columns per block
+#ifndef SFM_CONV_MINW
+#define SFM_CONV_MINW 2
+#endif
+constexpr int kTileY = 8;           // output rows per block
+constexpr int kHaloX = kTileX + 2;  // 66
+constexpr int kHaloY = kTileY + 2;  // 10
+constexpr int kInBytes = kHaloY * kHaloX * 64;  // one 32-channel chunk: 64 B per pixel
+constexpr int kWBytes = 9 * 32 * 64;            // 9 taps x 32 cout x 32 cin bf16
+constexpr int kConvThreads = 256;               // 4 waves: 2 row groups x 2 column halves
+constexpr int kInChunks = kHaloY * kHaloX * 4;  // 16-byte chunks per stage
+constexpr int kWChunks = 9 * 32 * 4;
+constexpr int kInPer = (kInChunks + kConvThreads - 1) / kConvThreads;  // per thread
+constexpr int kWPer = (kWChunks + kConvThreads - 1) / kConvThreads;
+
+__device__ __forceinline__ int swz(int chunk, int row) { return chunk ^ ((row >> 2) & 3); }
+
+__device__ __forceinline__ float bf2f(unsigned short b) { return __uint_as_float((unsigned int)b << 16); }
+
+__device__ __forceinline__ unsigned short f2bf(float f) {  // RNE (v_cvt_pk_bf16_f32)
+  const __bf16 v = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, v);
+}
+
+// D = W . X: rows = 32 output channels (weights as the A operand), columns =
+// 32 pixels of one output row (the input as the B operand).  A wave owns 4
+// output rows x 32 pixels (4 accumulators); each input row fragment it reads
+// from LDS feeds up to 3 of them (dy = 0, 1, 2), so an MFMA costs 0.5 input
+// and 0.25 weight ds_read_b128.
+__global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
+    const unsigned short* __restrict__ in, int cin, const unsigned short* __restrict__ wpk,
+    const float* __restrict__ scale, const float* __restrict__ bias, const unsigned short* __restrict__ res, int relu,
+    unsigned short* __restrict__ out, float* __restrict__ out1, int D, int H, int W) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds_in[kInBytes];
+  __shared__ __attribute__((aligned(16))) unsigned char lds_w[kWBytes];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int x0 = blockIdx.x * kTileX, y0 = blockIdx.y * kTileY;
+  const int d = blockIdx.z % D, b = blockIdx.z / D;
+  const int r = lane & 31, h = lane >> 5;
+  const int wrow = (wave >> 1) * 4, wcol = (wave & 1) * 32;
+  const int nchunk = cin >> 5;
+  const int nstage = 3 * nchunk;  // stage s: dz = s / nchunk, channel chunk cc = s % nchunk
+  const int64_t plane = (int64_t)H * W;
+
+  // register prefetch of one stage: global -> VGPRs during the previous stage's MFMAs
+  uint4 pin[kInPer], pw[kWPer];
+  auto fetch = [&](int s) {
+    const int dz = s / nchunk, cc = s - dz * nchunk;
+    const int zd = d + dz - 1;
+    const bool zin = zd >= 0 && zd < D;
+#pragma unroll
+    for (int k = 0; k < kInPer; ++k) {
+      const int i = tid + k * kConvThreads;
+      const int c = i & 3, px = (i >> 2) % kHaloX, ry = (i >> 2) / kHaloX;
+      const int gy = y0 - 1 + ry, gx = x0 - 1 + px;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (i < kInChunks && zin && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const int64_t pix = ((int64_t)b * D + zd) * plane + (int64_t)gy * W + gx;
+        v = *reinterpret_cast<const uint4*>(in + pix * cin + cc * 32 + c * 8);
+      }
+      pin[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) {
+      const int i = tid + k * kConvThreads;
+      const int c = i & 3, co = (i >> 2) & 31, t = i >> 7;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (i < kWChunks) v = *reinterpret_cast<const uint4*>(wpk + ((int64_t)(dz * 9 + t) * 32 + co) * cin + cc * 32 + c * 8);
+      pw[k] = v;
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < kInPer; ++k) {
+      const int i = tid + k * kConvThreads;
+      if (i < kInChunks) {
+        const int c = i & 3, px = (i >> 2) % kHaloX, ry = (i >> 2) / kHaloX;
+        *reinterpret_cast<uint4*>(lds_in + (ry * kHaloX + px) * 64 + swz(c, px) * 16) = pin[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) {
+      const int i = tid + k * kConvThreads;
+      if (i < kWChunks) {
+        const int c = i & 3, co = (i >> 2) & 31, t = i >> 7;
+        *reinterpret_cast<uint4*>(lds_w + (t * 32 + co) * 64 + swz(c, co) * 16) = pw[k];
+      }
+    }
+  };
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+    for (int i = 0; i < 16; ++i) acc[o][i] = 0.0f;
+
+  fetch(0);
+  for (int s = 0; s < nstage; ++s) {
+    __syncthreads();  // the previous stage's operand reads are done
+    commit();
+    __syncthreads();
+    if (s + 1 < nstage) fetch(s + 1);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int c = kb * 2 + h;
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        bf16x8 wf[3];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+          wf[dy] = *reinterpret_cast<const bf16x8*>(lds_w + ((dy * 3 + dx) * 32 + r) * 64 + swz(c, r) * 16);
+        const int p = wcol + r + dx;
+#pragma unroll
+        for (int ir = 0; ir < 6; ++ir) {  // input row wrow + ir of the halo
+          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
+#pragma unroll
+          for (int o = 0; o < 4; ++o) {
+            const int dy = ir - o;
+            if (dy >= 0 && dy <= 2) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[dy], xf, acc[o], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // epilogue: D[row = cout][col = pixel]; lane holds pixel r and couts 8q + 4h + (0..3) in acc[.][4q .. 4q+3]
+  const int x = x0 + wcol + r;
+  if (x >= W) return;
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const int y = y0 + wrow + o;
+    if (y >= H) break;
+    const int64_t pix = ((int64_t)b * D + d) * plane + (int64_t)y * W + x;
+    if (out1) {
+      if (h == 0) out1[pix] = __builtin_fmaf(acc[o][0], scale[0], bias[0]);
+      continue;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int co = 8 * q + 4 * h;
+      const float4 sc = *reinterpret_cast<const float4*>(scale + co);
+      const float4 bi = *reinterpret_cast<const float4*>(bias + co);
+      float v[4] = {__builtin_fmaf(acc[o][4 * q + 0], sc.x, bi.x), __builtin_fmaf(acc[o][4 * q + 1], sc.y, bi.y),
+                    __builtin_fmaf(acc[o][4 * q + 2], sc.z, bi.z), __builtin_fmaf(acc[o][4 * q + 3], sc.w, bi.w)};
+      if (relu)
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.0f);
+      if (res) {
+        const uint2 rv = *reinterpret_cast<const uint2*>(res + pix * 32 + co);
+        v[0] += bf2f(rv.x & 0xffff);
+        v[1] += bf2f(rv.x >> 16);
+        v[2] += bf2f(rv.y & 0xffff);
+        v[3] += bf2f(rv.y >> 16);
+      }
+      uint2 st;
+      st.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+      st.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(out + pix * 32 + co) = st;
+    }
+  }
+}
+
+// [B][C][P] (fp32 or bf16) -> [B][P][C] bf16, P = D*H*W.  A 64-pixel x C tile
+// through LDS: coalesced reads along P per channel, coalesced 16-byte writes.
+template <typename T>
+__global__ __launch_bounds__(256) void k_to_channels_last(const T* __restrict__ in, int C, int64_t P,
+                                                          unsigned short* __restrict__ out) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    __syncthreads();
+    for (int i = tid; i < 64 * 64; i += 256) {
+      const int px = i & 63, c = i >> 6;
+      const int64_t p = p0 + px;
+      float v = 0.0f;
+      if (p < P && c0 + c < C) {
+        if constexpr (sizeof(T) == 4) v = in[((int64_t)b * C + c0 + c) * P + p];
+        else v = bf2f(in[((int64_t)b * C + c0 + c) * P + p]);
+      }
+      tile[c][px] = v;
+    }
+    __syncthreads();
+    const int cw = min(64, C - c0);
+    for (int i = tid; i < 64 * (cw / 8); i += 256) {
+      const int g = i % (cw / 8), px = i / (cw / 8);
+      const int64_t p = p0 + px;
+      if (p >= P) continue;
+      unsigned short s[8];
+      for (int j = 0; j < 8; ++j) s[j] = f2bf(tile[g * 8 + j][px]);
+      uint4 v;
+      v.x = s[0] | ((unsigned)s[1] << 16);
+      v.y = s[2] | ((unsigned)s[3] << 16);
+      v.z = s[4] | ((unsigned)s[5] << 16);
+      v.w = s[6] | ((unsigned)s[7] << 16);
+      *reinterpret_cast<uint4*>(out + ((int64_t)b * P + p) * C + c0 + g * 8) = v;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace sfm
+
+using namespace sfm;
+
+extern "C" {
+
+int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, const void* weights,
+                   const float* scale, const float* bias, const void* residual, int relu, int cout, void* out,
+                   void* stream) {
+  SFM_REQUIRE(in && weights && scale && bias && out, "null pointer argument");
+  SFM_REQUIRE(cin == 32 || cin == 64, "cin must be 32 or 64");
+  SFM_REQUIRE(cout == 32 || cout == 1, "cout must be 32 or 1");
+  SFM_REQUIRE(cout == 32 || residual == nullptr, "residual needs cout 32");
+  SFM_REQUIRE(batch >= 1 && depth >= 1 && h >= 1 && w >= 1, "invalid conv shape");
+  SFM_REQUIRE((int64_t)batch * depth <= 65535 && (h + kTileY - 1) / kTileY <= 65535, "conv grid too large");
+  SFM_REQUIRE(in != out && (residual == nullptr || residual != out), "conv output must not alias its inputs");
+  SFM_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)weights & 15) == 0, "conv operands must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps("conv3", s);
+  dim3 grid((w + kTileX - 1) / kTileX, (h + kTileY - 1) / kTileY, batch * depth);
+  hipLaunchKernelGGL(k_conv3, grid, dim3(kConvThreads), 0, s, (const unsigned short*)in, cin, (const unsigned short*)weights,
+                     scale, bias, (const unsigned short*)residual, relu,
+                     cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w);
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
+                              void* stream) {
+  SFM_REQUIRE(in && out, "null pointer argument");
+  SFM_REQUIRE(in_dtype == 0 || in_dtype == 1, "in_dtype must be 0 (float32) or 1 (bfloat16)");
+  SFM_REQUIRE(batch >= 1 && batch <= 65535 && channels >= 8 && channels % 8 == 0 && plane >= 1,
+              "invalid channels-last shape (channels must be a multiple of 8)");
+  SFM_REQUIRE(((uintptr_t)out & 15) == 0, "output must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps("to_channels_last", s);
+  dim3 grid((unsigned)((plane + 63) / 64), batch);
+  if (in_dtype == 0)
+    hipLaunchKernelGGL(k_to_channels_last<float>, grid, dim3(256), 0, s, (const float*)in, channels, plane,
+                       (unsigned short*)out);
+  else
+    hipLaunchKernelGGL(k_to_channels_last<unsigned short>, grid, dim3(256), 0, s, (const unsigned short*)in, channels,
+                       plane, (unsigned short*)out);
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+}  // extern "C"

@@ -69,6 +69,11 @@ _SIGS = [
       ctypes.c_float, ctypes.c_float, _c_dp, _c_dp]),
     ("sfm_inverse_warp", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp]),
+    ("sfm_conv3_bf16", ctypes.c_int,
+     [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,
+      ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
+    ("sfm_to_channels_last_bf16", ctypes.c_int,
+     [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp]),
     ("sfm_tune_set", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("sfm_profile_enable", ctypes.c_int, [ctypes.c_int]),
     ("sfm_profile_reset", ctypes.c_int, []),

@@ -250,6 +250,28 @@ int sfm_inverse_warp(const float* feat, int batch, int channels, int h, int w,
                      const float* depth, const float* pose, const float* K, const float* Kinv,
                      float* out, void* stream);
 
+/* 3-D cost regularisation layer of PSNet (models/PSNet.py:79-102, applied at
+ * PSNet.py:159-165; convbn_3d = Conv3d(3, stride 1, pad 1, no bias) +
+ * BatchNorm3d, models/submodule.py:17-20), on the matrix cores in bf16 with
+ * fp32 accumulation:
+ *   out = [relu](conv3x3x3(in) * scale[co] + bias[co]) [+ residual]
+ *   in [dev] batch x depth x h x w x cin bf16 (channels-last), cin 32 or 64;
+ *   weights [dev] 27 x 32 x cin bf16, tap = (kd*3 + kh)*3 + kw, cout
+ *     zero-padded to 32 when cout == 1;
+ *   scale, bias [dev] 32 float32 (BatchNorm folded; 1 / 0 for a plain conv);
+ *   residual [dev] like out or NULL (cout 32 only), added after the ReLU;
+ *   out [dev] batch x depth x h x w x 32 bf16 (cout 32), or
+ *       batch x depth x h x w float32 (cout 1: the classify output). */
+int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, const void* weights,
+                   const float* scale, const float* bias, const void* residual, int relu, int cout, void* out,
+                   void* stream);
+
+/* [batch][channels][plane] float32 (in_dtype 0) or bfloat16 (1) ->
+ * [batch][plane][channels] bfloat16 (channels a multiple of 8): the
+ * sweep's cost volume [B, 2C, L, h, w] into sfm_conv3_bf16's layout. */
+int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
+                              void* stream);
+
 /* Launch-shape tuning (process-wide): "solve_lanes" (1..64, default 32),
  * "sweep_items_per_block" (1, 2, 4 or 8; default 4), "sweep_lane_pixels"
  * (0/1, pixel-to-lane mapping of the warped rows), "score_blocks_per_cu"
