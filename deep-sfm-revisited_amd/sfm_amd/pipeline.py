@@ -45,8 +45,15 @@ class TwoViewHotPath:
         self.cost_dtype = cost_dtype
         self.sweep_ws = sweep.workspace_for(B, self.C, self.h, self.w, self.device)
 
-    def pose(self, flow, K):
-        Kinv = torch.inverse(K.float())
+    @staticmethod
+    def k_inverse(K):
+        """K^-1 without a host sync: linalg.inv_ex is torch.inverse's own LU
+        solve minus the singularity check that blocks on the device."""
+        return torch.linalg.inv_ex(K.float())[0]
+
+    def pose(self, flow, K, Kinv=None):
+        if Kinv is None:
+            Kinv = self.k_inverse(K)
         if self.fused:
             return ransac.ransac5_flow(flow, Kinv, self.iters, self.thr, self.H, self.W, self.margin, seed=self.seed,
                                        workspace=self.ws)
@@ -55,8 +62,9 @@ class TwoViewHotPath:
                                                 True, workspace=self.ws)
         return E, P, inl, win
 
-    def sweep(self, ref_fea, tgt_fea, P, K):
-        Kinv = torch.inverse(K.float())
+    def sweep(self, ref_fea, tgt_fea, P, K, Kinv=None):
+        if Kinv is None:
+            Kinv = self.k_inverse(K)
         K4, Ki4 = sweep.quarter_intrinsics(K.float(), Kinv)
         pose = P.float()
         if self.rescale is not None:
@@ -65,6 +73,7 @@ class TwoViewHotPath:
                                       out=self.cost, workspace=self.sweep_ws)
 
     def step(self, flow, K, ref_fea, tgt_fea):
-        E, P, inl, win = self.pose(flow, K)
-        cost = self.sweep(ref_fea, tgt_fea, P, K)
+        Kinv = self.k_inverse(K)
+        E, P, inl, win = self.pose(flow, K, Kinv)
+        cost = self.sweep(ref_fea, tgt_fea, P, K, Kinv)
         return E, P, inl, cost
