@@ -142,6 +142,33 @@ static size_t corr_ws_bytes(int B, int C, int h, int w) {
   return 2 * ((quads + 255) & ~(size_t)255);
 }
 
+// Flow2Depth (models/flow2depth.py:7-41; dead code in the reference, kept
+// for the API).  vec_p = (K R) dir_p + K T with dir_p = float32(Ki (j, i, 1))
+// formed in float64 as numpy does (float32 Ki times int64 pixel -> float64).
+// The reference views the [B, H*W, 3] result as [B, 3, H, W] and returns
+// channel 2, i.e. flat element 2HW + k of each batch's buffer: out[b, k] =
+// vec_p[c] with p = (2HW + k) / 3, c = (2HW + k) % 3.
+constexpr int kF2DThreads = 256;
+__global__ __launch_bounds__(kF2DThreads) void k_flow2depth(const float* __restrict__ KR, const float* __restrict__ KT,
+                                                            const float* __restrict__ Ki, int H, int W,
+                                                            float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int64_t hw = (int64_t)H * W;
+  const int64_t k = (int64_t)blockIdx.x * kF2DThreads + threadIdx.x;
+  if (k >= hw) return;
+  const int64_t f = 2 * hw + k;
+  const int64_t p = f / 3;
+  const int c = (int)(f - 3 * p);
+  const int i = (int)(p / W), j = (int)(p - (int64_t)i * W);
+  const float* ki = Ki + 9 * b;
+  float dir[3];
+  for (int r = 0; r < 3; ++r)
+    dir[r] = (float)(((double)ki[3 * r] * (double)j + (double)ki[3 * r + 1] * (double)i) + (double)ki[3 * r + 2]);
+  const float* kr = KR + 9 * b + 3 * c;
+  const float first = (kr[0] * dir[0] + kr[1] * dir[1]) + kr[2] * dir[2];
+  out[b * hw + k] = first + KT[3 * b + c];
+}
+
 }  // namespace sfm
 
 using namespace sfm;
@@ -208,3 +235,17 @@ int sfm_depth_head(const float* cost, int batch, int nlabel, int h, int w, int H
 }
 
 }  // extern "C"
+
+extern "C" int sfm_flow2depth(const float* KR, const float* KT, const float* Kinv, int batch, int H, int W, float* out,
+                              void* stream) {
+  SFM_REQUIRE(KR && KT && Kinv && out, "null pointer argument");
+  SFM_REQUIRE(batch >= 1 && batch <= 65535 && H >= 1 && W >= 1 && (int64_t)H * W < ((int64_t)1 << 31) / 3,
+              "invalid flow2depth shape");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps("flow2depth", s);
+  const int64_t hw = (int64_t)H * W;
+  hipLaunchKernelGGL(k_flow2depth, dim3((unsigned)((hw + kF2DThreads - 1) / kF2DThreads), batch), dim3(kF2DThreads), 0,
+                     s, KR, KT, Kinv, H, W, out);
+  SFM_LAUNCHED();
+  return SFM_OK;
+}

@@ -133,3 +133,27 @@ class SweepDepthEstimator(torch.nn.Module):
         cost = cost / len(targets)
         depth = depth_head(cost, self.nlabel, self.mindepth, (ref.shape[2], ref.shape[3]), self.predict_by_depth)
         return depth, depth
+
+
+def flow2depth(R, T, initial_flow, K_mat):
+    """Flow2Depth(R, T, initial_flow, K_mat) of models/flow2depth.py:7-41 ->
+    [B, H, W] float32 on the flow's device.  The flow is read for its shape
+    only, as in the reference.  K^-1 is numpy's inverse of K (float32, as
+    the reference computes it on the host); K.R and K.T are torch matmuls.
+    Unlike the reference (whose pixel loop only works for B = 1) any batch
+    size is accepted, each pair with its own K."""
+    import numpy as np
+    B, _, H, W = initial_flow.shape
+    dev = initial_flow.device
+    if not initial_flow.is_cuda:
+        raise RuntimeError("flow2depth needs a device flow tensor (HIP path, no CPU fallback)")
+    Kd = K_mat.to(dev, torch.float32).reshape(B, 3, 3)
+    KR = torch.matmul(Kd, R.to(dev, torch.float32).reshape(B, 3, 3)).contiguous()
+    KT = torch.matmul(Kd, T.to(dev, torch.float32).reshape(B, 3, 1)).reshape(B, 3).contiguous()
+    Ki = torch.from_numpy(np.linalg.inv(K_mat.detach().cpu().numpy().reshape(B, 3, 3))).to(dev, torch.float32)
+    out = torch.empty(B, H, W, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        rc = _lib.load().sfm_flow2depth(_lib.ptr(KR), _lib.ptr(KT), _lib.ptr(Ki.contiguous()), B, H, W,
+                                        _lib.ptr(out), _lib.stream_ptr(dev))
+        _lib.check(rc, "sfm_flow2depth")
+    return out

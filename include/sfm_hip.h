@@ -250,6 +250,14 @@ int sfm_inverse_warp(const float* feat, int batch, int channels, int h, int w,
                      const float* depth, const float* pose, const float* K, const float* Kinv,
                      float* out, void* stream);
 
+/* Flow2Depth, models/flow2depth.py:7-41 (dead code in the reference):
+ *   KR = K.R [dev] B x 3 x 3, KT = K.T [dev] B x 3, Kinv [dev] B x 3 x 3
+ *   (float32, numpy's inverse of K as the reference takes it);
+ *   out [dev] B x H x W float32 = channel 2 of the [B, H*W, 3] result viewed
+ *   as [B, 3, H, W], exactly as the reference returns it. */
+int sfm_flow2depth(const float* KR, const float* KT, const float* Kinv, int batch, int H, int W, float* out,
+                   void* stream);
+
 /* 3-D cost regularisation layer of PSNet (models/PSNet.py:79-102, applied at
  * PSNet.py:159-165; convbn_3d = Conv3d(3, stride 1, pad 1, no bias) +
  * BatchNorm3d, models/submodule.py:17-20), on the matrix cores in bf16 with

@@ -55,3 +55,30 @@ def test_correlation_depth_module(cuda):
     want = S.depth_head(cost, L, 1.0, (4 * h, 4 * w))
     rel = ((got - want).abs() / want.abs()).max()
     assert float(rel) <= 1e-4, float(rel)
+
+
+def test_flow2depth_golden(cuda, golden):
+    # models/flow2depth.py run by the reference itself (tests/golden/warp.npz)
+    from sfm_amd.depth import flow2depth
+    g = golden("warp.npz")["flow2depth"]
+    flow = torch.zeros(*g["shape"].tolist(), device=cuda)
+    got = flow2depth(torch.from_numpy(g["R"]), torch.from_numpy(g["T"]), flow, torch.from_numpy(g["K"])).cpu()
+    want = torch.from_numpy(g["out"])
+    assert got.shape == want.shape
+    err = (got - want).abs() - (1e-5 * want.abs() + 1e-5)
+    assert float(err.max()) <= 0, float((got - want).abs().max())
+
+
+@pytest.mark.parametrize("H,W", [(37, 53), (376, 1242)])
+def test_flow2depth_vs_oracle(cuda, H, W):
+    from sfm_amd import synth
+    from sfm_amd.depth import flow2depth
+    pose = synth.relative_pose(1, torch.Generator().manual_seed(H)).float()
+    K = synth.intrinsics(1)
+    R, T = pose[:, :, :3], pose[:, :, 3]
+    got = flow2depth(R, T, torch.zeros(1, 2, H, W, device=cuda), K).cpu()
+    want = S.flow2depth(R, T, torch.zeros(1, 2, H, W), K)
+    # fp32 sums of O(1e3) terms in another order; near-cancelling outputs keep
+    # the operands' absolute rounding (a few ulp of max|out|)
+    err = (got - want).abs() - (1e-5 * want.abs() + 1e-6 * float(want.abs().max()))
+    assert float(err.max()) <= 0, float((got - want).abs().max())
