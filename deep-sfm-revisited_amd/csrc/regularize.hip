@@ -39,10 +39,7 @@ constexpr int kHaloY = kTileY + 2;  // 10
 constexpr int kInBytes = kHaloY * kHaloX * 64;  // one 32-channel chunk: 64 B per pixel
 constexpr int kWBytes = 9 * 32 * 64;            // 9 taps x 32 cout x 32 cin bf16
 constexpr int kConvThreads = 256;               // 4 waves: 2 row groups x 2 column halves
-constexpr int kInChunks = kHaloY * kHaloX * 4;  // 16-byte chunks per stage
-constexpr int kWChunks = 9 * 32 * 4;
-constexpr int kInPer = (kInChunks + kConvThreads - 1) / kConvThreads;  // per thread
-constexpr int kWPer = (kWChunks + kConvThreads - 1) / kConvThreads;
+static_assert(kConvThreads == 4 * kTileX && kHaloY * 8 <= kConvThreads, "staging map: 4 chunks x 64 columns");
 
 __device__ __forceinline__ int swz(int chunk, int row) { return chunk ^ ((row >> 2) & 3); }
 
@@ -74,50 +71,60 @@ __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
   const int nstage = 3 * nchunk;  // stage s: dz = s / nchunk, channel chunk cc = s % nchunk
   const int64_t plane = (int64_t)H * W;
 
-  // register prefetch of one stage: global -> VGPRs during the previous stage's MFMAs
-  uint4 pin[kInPer], pw[kWPer];
+  // Register prefetch of one stage (global -> VGPRs during the previous
+  // stage's MFMAs).  Thread t stages chunk t&3 of halo column t>>2 (0..63)
+  // in all 10 halo rows, threads < 80 also one chunk of columns 64/65, and
+  // 4-5 weight chunks.  Every per-thread address part is hoisted out of the
+  // stage loop; a stage only moves scalar plane / row / chunk bases.
+  const int mc = tid & 3, mpx = tid >> 2;
+  const int mgx = x0 - 1 + mpx;
+  const bool mvx = mgx >= 0 && mgx < W;
+  const int moff = mgx * cin + mc * 8;
+  const int mlds = mpx * 64 + swz(mc, mpx) * 16;
+  const bool hasx = tid < kHaloY * 8;
+  const int epx = 64 + ((tid >> 2) & 1), ery = tid >> 3;
+  const int egx = x0 - 1 + epx, egy = y0 - 1 + ery;
+  const bool evalid = hasx && egx < W && egy >= 0 && egy < H;
+  const int eoff = egy * W * cin + egx * cin + mc * 8;
+  const int elds = (ery * kHaloX + epx) * 64 + swz(mc, epx) * 16;
+  const int wco = (tid >> 2) & 31, wt0 = tid >> 7;
+  const int woff = (wt0 * 32 + wco) * cin + mc * 8;
+  const int wlds = (wt0 * 32 + wco) * 64 + swz(mc, wco) * 16;
+  const int rowstride = W * cin;
+  uint4 pin[kHaloY + 1], pw[5];
   auto fetch = [&](int s) {
     const int dz = s / nchunk, cc = s - dz * nchunk;
     const int zd = d + dz - 1;
     const bool zin = zd >= 0 && zd < D;
+    const unsigned short* pl = in + (((int64_t)b * D + (zin ? zd : 0)) * plane) * cin + cc * 32;
 #pragma unroll
-    for (int k = 0; k < kInPer; ++k) {
-      const int i = tid + k * kConvThreads;
-      const int c = i & 3, px = (i >> 2) % kHaloX, ry = (i >> 2) / kHaloX;
-      const int gy = y0 - 1 + ry, gx = x0 - 1 + px;
+    for (int ry = 0; ry < kHaloY; ++ry) {
+      const int gy = y0 - 1 + ry;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (i < kInChunks && zin && gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        const int64_t pix = ((int64_t)b * D + zd) * plane + (int64_t)gy * W + gx;
-        v = *reinterpret_cast<const uint4*>(in + pix * cin + cc * 32 + c * 8);
-      }
-      pin[k] = v;
+      if (zin && gy >= 0 && gy < H && mvx) v = *reinterpret_cast<const uint4*>(pl + gy * rowstride + moff);
+      pin[ry] = v;
     }
-#pragma unroll
-    for (int k = 0; k < kWPer; ++k) {
-      const int i = tid + k * kConvThreads;
-      const int c = i & 3, co = (i >> 2) & 31, t = i >> 7;
+    {
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (i < kWChunks) v = *reinterpret_cast<const uint4*>(wpk + ((int64_t)(dz * 9 + t) * 32 + co) * cin + cc * 32 + c * 8);
+      if (zin && evalid) v = *reinterpret_cast<const uint4*>(pl + eoff);
+      pin[kHaloY] = v;
+    }
+    const unsigned short* wb = wpk + (int64_t)dz * 9 * 32 * cin + cc * 32;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (wt0 + 2 * k < 9) v = *reinterpret_cast<const uint4*>(wb + woff + k * 2 * 32 * cin);
       pw[k] = v;
     }
   };
   auto commit = [&]() {
 #pragma unroll
-    for (int k = 0; k < kInPer; ++k) {
-      const int i = tid + k * kConvThreads;
-      if (i < kInChunks) {
-        const int c = i & 3, px = (i >> 2) % kHaloX, ry = (i >> 2) / kHaloX;
-        *reinterpret_cast<uint4*>(lds_in + (ry * kHaloX + px) * 64 + swz(c, px) * 16) = pin[k];
-      }
-    }
+    for (int ry = 0; ry < kHaloY; ++ry)
+      *reinterpret_cast<uint4*>(lds_in + ry * kHaloX * 64 + mlds) = pin[ry];
+    if (hasx) *reinterpret_cast<uint4*>(lds_in + elds) = pin[kHaloY];
 #pragma unroll
-    for (int k = 0; k < kWPer; ++k) {
-      const int i = tid + k * kConvThreads;
-      if (i < kWChunks) {
-        const int c = i & 3, co = (i >> 2) & 31, t = i >> 7;
-        *reinterpret_cast<uint4*>(lds_w + (t * 32 + co) * 64 + swz(c, co) * 16) = pw[k];
-      }
-    }
+    for (int k = 0; k < 5; ++k)
+      if (wt0 + 2 * k < 9) *reinterpret_cast<uint4*>(lds_w + wlds + k * 2 * 32 * 64) = pw[k];
   };
 
   f32x16 acc[4];
@@ -136,20 +143,19 @@ __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
       const int c = kb * 2 + h;
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
-        bf16x8 wf[3];
+        bf16x8 wf[3], xf[6];
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
           wf[dy] = *reinterpret_cast<const bf16x8*>(lds_w + ((dy * 3 + dx) * 32 + r) * 64 + swz(c, r) * 16);
         const int p = wcol + r + dx;
 #pragma unroll
-        for (int ir = 0; ir < 6; ++ir) {  // input row wrow + ir of the halo
-          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
+        for (int ir = 0; ir < 6; ++ir)  // input rows wrow .. wrow + 5 of the halo
+          xf[ir] = *reinterpret_cast<const bf16x8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
+        // dy-major: consecutive MFMAs update different accumulators
 #pragma unroll
-          for (int o = 0; o < 4; ++o) {
-            const int dy = ir - o;
-            if (dy >= 0 && dy <= 2) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[dy], xf, acc[o], 0, 0, 0);
-          }
-        }
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int o = 0; o < 4; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[dy], xf[o + dy], acc[o], 0, 0, 0);
       }
     }
   }
@@ -245,6 +251,7 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
   SFM_REQUIRE(cout == 32 || residual == nullptr, "residual needs cout 32");
   SFM_REQUIRE(batch >= 1 && depth >= 1 && h >= 1 && w >= 1, "invalid conv shape");
   SFM_REQUIRE((int64_t)batch * depth <= 65535 && (h + kTileY - 1) / kTileY <= 65535, "conv grid too large");
+  SFM_REQUIRE((int64_t)h * w * cin < ((int64_t)1 << 31), "conv plane too large (32-bit in-plane offsets)");
   SFM_REQUIRE(in != out && (residual == nullptr || residual != out), "conv output must not alias its inputs");
   SFM_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)weights & 15) == 0, "conv operands must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
