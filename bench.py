@@ -36,6 +36,7 @@ from sfm_amd.pipeline import TwoViewHotPath  # noqa: E402
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP64_TFLOPS = 78.6      # MI355X fp64 vector spec
 PEAK_FP32_TFLOPS = 157.3     # MI355X fp32 vector spec (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0    # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 FLOP_PER_EVAL = 50           # Ex, xE, x'Ex, sqrt, div, |.|
 
 
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--threshold", type=float, default=1e-4)
     ap.add_argument("--cost-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-regularize", action="store_true",
+                    help="skip the (unscored) PSNet 3-D regularisation roofline line after the timed region")
     ap.add_argument("--fused", action="store_true",
                     help="RANSAC reads the flow directly (sfm_ransac5_flow) instead of materialised correspondences")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -101,6 +104,36 @@ def cpu_baseline(flow, K, ref_fea, tgt_fea, pose, args):
             "sample": (f"1 KITTI pair: RANSAC {chains}/512 chains x {args.iters} iters on N=435032 "
                        f"({t_ransac:.2f} s/pair scaled), sweep {len(planes)}/{args.nlabel} planes "
                        f"({t_sweep:.3f} s/pair scaled), oracle C++ (OpenMP) + torch-CPU fp32")}
+
+
+def regularize_roofline(cost, steps=3):
+    """PSNet's 12-layer 3-D cost regularisation (sfm_conv3_bf16) on the first
+    pair of the last step's cost volume, after the timed region.  Not part of
+    ``value`` (the metric's path ends at the cost volume); reported so the
+    MFMA kernel's roofline is measured live beside the path's."""
+    from sfm_amd.regularize import CostRegularization
+    torch.manual_seed(0)
+    reg = CostRegularization(cost.shape[1]).to(cost.device).eval()
+    one = cost[:1]
+    reg(one)
+    torch.cuda.synchronize(cost.device)
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    for _ in range(steps):
+        reg(one)
+    torch.cuda.synchronize(cost.device)
+    _lib.profile_enable(False)
+    ms, n = _lib.profile_read("conv3")
+    _, L, h, w = one.shape[1:]
+    vox = L * h * w
+    flop = 2 * vox * 27 * (one.shape[1] * 32 + 10 * 32 * 32 + 32)
+    per_stack = ms / steps
+    tf = flop / (per_stack * 1e-3) / 1e12
+    return {"kernel": "conv3 x12 (PSNet dres0..classify, bf16 MFMA)", "bound": "mfma-bf16", "achieved": round(tf, 1),
+            "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4),
+            "avg_launch_ms": round(ms / max(n, 1), 4), "ms_per_stack": round(per_stack, 4),
+            "work": f"{flop} FLOP per stack (1 pair, L={L}, {h}x{w}; 2*27*Cin*Cout per voxel and layer)",
+            "note": "not part of value: the CNN after the measured path, timed after it"}
 
 
 def main():
@@ -190,6 +223,11 @@ def main():
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "inliers": [int(v) for v in inl.cpu()],
         }
+        if not args.no_regularize and hp.cost.dtype in (torch.float32, torch.bfloat16):
+            try:
+                out["roofline_regularize"] = regularize_roofline(hp.cost)
+            except Exception as e:   # extra information, never the metric
+                out["roofline_regularize"] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(flow, K, ref_fea, tgt_fea, P.float(), args)

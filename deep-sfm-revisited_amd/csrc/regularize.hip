@@ -30,6 +30,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kTileX = 64;          // output columns per block
+constexpr int kXcds = 8;            // MI355X: 8 XCDs, each with its own L2
 #ifndef SFM_CONV_MINW
 #define SFM_CONV_MINW 2
 #endif
@@ -58,13 +59,26 @@ __device__ __forceinline__ unsigned short f2bf(float f) {  // RNE (v_cvt_pk_bf16
 __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
     const unsigned short* __restrict__ in, int cin, const unsigned short* __restrict__ wpk,
     const float* __restrict__ scale, const float* __restrict__ bias, const unsigned short* __restrict__ res, int relu,
-    unsigned short* __restrict__ out, float* __restrict__ out1, int D, int H, int W) {
+    unsigned short* __restrict__ out, float* __restrict__ out1, int D, int H, int W, int ntx, int nty, int nblk,
+    int per_xcd) {
   __shared__ __attribute__((aligned(16))) unsigned char lds_in[kInBytes];
   __shared__ __attribute__((aligned(16))) unsigned char lds_w[kWBytes];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int x0 = blockIdx.x * kTileX, y0 = blockIdx.y * kTileY;
-  const int d = blockIdx.z % D, b = blockIdx.z / D;
+  // XCD-aware order: the dispatcher deals workgroup ids round-robin over the
+  // 8 XCDs, so id % 8 picks the XCD and id / 8 the slot on it.  Logical
+  // blocks are d-fastest, and each XCD owns a contiguous logical range: the
+  // blocks resident on one XCD at a time are consecutive depth slices of one
+  // (x, y) tile, which stage the same input planes (d-1, d, d+1) and so hit
+  // each other's lines in that XCD's L2 instead of re-reading HBM 3 times.
+  const int logical = (int)(blockIdx.x % kXcds) * per_xcd + (int)(blockIdx.x / kXcds);
+  if (logical >= nblk) return;  // whole block, before any barrier
+  const int d = logical % D;
+  int rest = logical / D;
+  const int tx = rest % ntx;
+  rest /= ntx;
+  const int ty = rest % nty, b = rest / nty;
+  const int x0 = tx * kTileX, y0 = ty * kTileY;
   const int r = lane & 31, h = lane >> 5;
   const int wrow = (wave >> 1) * 4, wcol = (wave & 1) * 32;
   const int nchunk = cin >> 5;
@@ -250,16 +264,19 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
   SFM_REQUIRE(cout == 32 || cout == 1, "cout must be 32 or 1");
   SFM_REQUIRE(cout == 32 || residual == nullptr, "residual needs cout 32");
   SFM_REQUIRE(batch >= 1 && depth >= 1 && h >= 1 && w >= 1, "invalid conv shape");
-  SFM_REQUIRE((int64_t)batch * depth <= 65535 && (h + kTileY - 1) / kTileY <= 65535, "conv grid too large");
   SFM_REQUIRE((int64_t)h * w * cin < ((int64_t)1 << 31), "conv plane too large (32-bit in-plane offsets)");
   SFM_REQUIRE(in != out && (residual == nullptr || residual != out), "conv output must not alias its inputs");
   SFM_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)weights & 15) == 0, "conv operands must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps("conv3", s);
-  dim3 grid((w + kTileX - 1) / kTileX, (h + kTileY - 1) / kTileY, batch * depth);
-  hipLaunchKernelGGL(k_conv3, grid, dim3(kConvThreads), 0, s, (const unsigned short*)in, cin, (const unsigned short*)weights,
-                     scale, bias, (const unsigned short*)residual, relu,
-                     cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w);
+  const int ntx = (w + kTileX - 1) / kTileX, nty = (h + kTileY - 1) / kTileY;
+  const int64_t nblk = (int64_t)ntx * nty * batch * depth;
+  SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
+  const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
+  hipLaunchKernelGGL(k_conv3, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, (const unsigned short*)in, cin,
+                     (const unsigned short*)weights, scale, bias, (const unsigned short*)residual, relu,
+                     cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w, ntx,
+                     nty, (int)nblk, per_xcd);
   SFM_LAUNCHED();
   return SFM_OK;
 }
