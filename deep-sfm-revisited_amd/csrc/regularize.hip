@@ -22,6 +22,7 @@
 // fp32 and stores bf16 four channels at a time (or, for the last layer, the
 // single output channel as fp32 [B][D][H][W], the layout the depth head reads).
 #include "common.h"
+#include <type_traits>
 
 namespace sfm {
 namespace {
@@ -210,6 +211,197 @@ __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
   }
 }
 
+// k_conv3r: the cin = 32 layers, rolling along the depth (plane) axis.  A
+// block owns a 4-row x 64-column tile for kPlanes consecutive output planes.
+// All 27 weight taps stay resident in LDS (54 KB, staged once per block) and
+// every input plane of the range is staged ONCE (6 x 66 halo, 25 KB): plane
+// z feeds output planes z+1, z and z-1 (dz = 0, 1, 2) from three rotating
+// accumulator sets, and plane z-1 is complete (stored) after plane z.  This
+// cuts the bytes a CU pulls from L2/HBM per MFMA ~3.6x against k_conv3,
+// whose per-CU load rate (~8 B/cycle) was the binding limit (PMC).
+// A wave owns 2 rows x 32 columns: 3 planes x 2 rows = six 32x32 accumulators.
+constexpr int kPlanes = 8;                          // output planes per block
+constexpr int kRTileY = 4;                          // output rows per block
+constexpr int kRHaloY = kRTileY + 2;                // 6
+constexpr int kRInBytes = kRHaloY * kHaloX * 64;    // 25,344
+constexpr int kRWBytes = 27 * 32 * 64;              // 55,296
+constexpr int kRLds = kRInBytes + kRWBytes;         // 80,640: two blocks per CU
+
+__global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restrict__ in,
+                                                   const unsigned short* __restrict__ wpk,
+                                                   const float* __restrict__ scale, const float* __restrict__ bias,
+                                                   const unsigned short* __restrict__ res, int relu,
+                                                   unsigned short* __restrict__ out, float* __restrict__ out1, int D,
+                                                   int H, int W, int ntx, int nty, int ndc, int nblk, int per_xcd) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned char* lds_w = lds;
+  unsigned char* lds_in = lds + kRWBytes;
+  const int logical = (int)(blockIdx.x % kXcds) * per_xcd + (int)(blockIdx.x / kXcds);
+  if (logical >= nblk) return;  // whole block, before any barrier
+  int rest = logical;
+  const int dc = rest % ndc;
+  rest /= ndc;
+  const int tx = rest % ntx;
+  rest /= ntx;
+  const int ty = rest % nty, b = rest / nty;
+  const int x0 = tx * kTileX, y0 = ty * kRTileY, d0 = dc * kPlanes;
+  const int nd = min(kPlanes, D - d0);  // output planes of this block
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wrow = (wave >> 1) * 2, wcol = (wave & 1) * 32;
+  const int64_t plane = (int64_t)H * W;
+  constexpr int cin = 32;
+
+  // all 27 taps of the weights, once: [tap][cout][32 cin] swizzled
+  for (int i = tid; i < 27 * 32 * 4; i += 256) {
+    const int c = i & 3, co = (i >> 2) & 31, t = i >> 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(wpk + (t * 32 + co) * cin + c * 8);
+    *reinterpret_cast<uint4*>(lds_w + (t * 32 + co) * 64 + swz(c, co) * 16) = v;
+  }
+
+  // input staging map (hoisted): chunk t&3 of halo column t>>2 in all 6 rows;
+  // threads < 48 also one chunk of columns 64/65
+  const int mc = tid & 3, mpx = tid >> 2;
+  const int mgx = x0 - 1 + mpx;
+  const bool mvx = mgx >= 0 && mgx < W;
+  const int moff = mgx * cin + mc * 8;
+  const int mlds = mpx * 64 + swz(mc, mpx) * 16;
+  const bool hasx = tid < kRHaloY * 8;
+  const int epx = 64 + ((tid >> 2) & 1), ery = tid >> 3;
+  const int egx = x0 - 1 + epx, egy = y0 - 1 + ery;
+  const bool evalid = hasx && egx < W && egy >= 0 && egy < H;
+  const int eoff = egy * W * cin + egx * cin + mc * 8;
+  const int elds = (ery * kHaloX + epx) * 64 + swz(mc, epx) * 16;
+  const int rowstride = W * cin;
+  uint4 pin[kRHaloY + 1];
+  auto fetch = [&](int z) {
+    const bool zin = z >= 0 && z < D;
+    const unsigned short* pl = in + (((int64_t)b * D + (zin ? z : 0)) * plane) * cin;
+#pragma unroll
+    for (int ry = 0; ry < kRHaloY; ++ry) {
+      const int gy = y0 - 1 + ry;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (zin && gy >= 0 && gy < H && mvx) v = *reinterpret_cast<const uint4*>(pl + gy * rowstride + moff);
+      pin[ry] = v;
+    }
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (zin && evalid) v = *reinterpret_cast<const uint4*>(pl + eoff);
+    pin[kRHaloY] = v;
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int ry = 0; ry < kRHaloY; ++ry) *reinterpret_cast<uint4*>(lds_in + ry * kHaloX * 64 + mlds) = pin[ry];
+    if (hasx) *reinterpret_cast<uint4*>(lds_in + elds) = pin[kRHaloY];
+  };
+
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+      for (int i = 0; i < 16; ++i) acc[k][o][i] = 0.0f;
+
+  auto store = [&](f32x16* a, int d) {  // epilogue of output plane d (rows wrow, wrow+1)
+    const int x = x0 + wcol + r;
+    if (x >= W) return;
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const int y = y0 + wrow + o;
+      if (y >= H) break;
+      const int64_t pix = ((int64_t)b * D + d) * plane + (int64_t)y * W + x;
+      if (out1) {
+        if (h == 0) out1[pix] = __builtin_fmaf(a[o][0], scale[0], bias[0]);
+        continue;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = 8 * q + 4 * h;
+        const float4 sc = *reinterpret_cast<const float4*>(scale + co);
+        const float4 bi = *reinterpret_cast<const float4*>(bias + co);
+        float v[4] = {__builtin_fmaf(a[o][4 * q + 0], sc.x, bi.x), __builtin_fmaf(a[o][4 * q + 1], sc.y, bi.y),
+                      __builtin_fmaf(a[o][4 * q + 2], sc.z, bi.z), __builtin_fmaf(a[o][4 * q + 3], sc.w, bi.w)};
+        if (relu)
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.0f);
+        if (res) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(res + pix * 32 + co);
+          v[0] += bf2f(rv.x & 0xffff);
+          v[1] += bf2f(rv.x >> 16);
+          v[2] += bf2f(rv.y & 0xffff);
+          v[3] += bf2f(rv.y >> 16);
+        }
+        uint2 st;
+        st.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+        st.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(out + pix * 32 + co) = st;
+      }
+    }
+  };
+
+  // step j stages plane z = d0 - 1 + j and feeds output planes m = j - dz
+  // (m in [0, nd)); ring slot of output m is m % 3, i.e. (PH - dz) mod 3.
+  const int nsteps = nd + 2;
+  auto step = [&](auto ph, int j) {
+    constexpr int PH = decltype(ph)::value;
+    __syncthreads();  // previous plane's operand reads are done
+    commit();
+    __syncthreads();
+    if (j + 1 < nsteps) fetch(d0 + j);  // plane of step j + 1
+    const bool v0 = j < nd, v1 = j >= 1 && j - 1 < nd, v2 = j >= 2;
+#pragma unroll
+    for (int g = 0; g < 6; ++g) {
+      const int kb = g / 3, dx = g - 3 * (g / 3);
+      const int c = kb * 2 + h;
+      bf16x8 wf[3][3], xf[4];
+#pragma unroll
+      for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+          wf[dz][dy] = *reinterpret_cast<const bf16x8*>(lds_w + (((dz * 3 + dy) * 3 + dx) * 32 + r) * 64 + swz(c, r) * 16);
+      const int p = wcol + r + dx;
+#pragma unroll
+      for (int ir = 0; ir < 4; ++ir)
+        xf[ir] = *reinterpret_cast<const bf16x8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
+      if (v0) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int o = 0; o < 2; ++o)
+            acc[PH][o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[0][dy], xf[o + dy], acc[PH][o], 0, 0, 0);
+      }
+      if (v1) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int o = 0; o < 2; ++o)
+            acc[(PH + 2) % 3][o] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[1][dy], xf[o + dy], acc[(PH + 2) % 3][o], 0, 0, 0);
+      }
+      if (v2) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int o = 0; o < 2; ++o)
+            acc[(PH + 1) % 3][o] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[2][dy], xf[o + dy], acc[(PH + 1) % 3][o], 0, 0, 0);
+      }
+    }
+    if (v2) {  // output plane m = j - 2 is complete
+      store(acc[(PH + 1) % 3], d0 + j - 2);
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+        for (int i = 0; i < 16; ++i) acc[(PH + 1) % 3][o][i] = 0.0f;
+    }
+  };
+
+  fetch(d0 - 1);
+  for (int j0 = 0; j0 < nsteps; j0 += 3) {
+    step(std::integral_constant<int, 0>{}, j0);
+    if (j0 + 1 < nsteps) step(std::integral_constant<int, 1>{}, j0 + 1);
+    if (j0 + 2 < nsteps) step(std::integral_constant<int, 2>{}, j0 + 2);
+  }
+}
+
 // [B][C][P] (fp32 or bf16) -> [B][P][C] bf16, P = D*H*W.  A 64-pixel x C tile
 // through LDS: coalesced reads along P per channel, coalesced 16-byte writes.
 template <typename T>
@@ -269,14 +461,31 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
   SFM_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)weights & 15) == 0, "conv operands must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
   ProfScope ps("conv3", s);
-  const int ntx = (w + kTileX - 1) / kTileX, nty = (h + kTileY - 1) / kTileY;
-  const int64_t nblk = (int64_t)ntx * nty * batch * depth;
-  SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
-  const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
-  hipLaunchKernelGGL(k_conv3, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, (const unsigned short*)in, cin,
-                     (const unsigned short*)weights, scale, bias, (const unsigned short*)residual, relu,
-                     cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w, ntx,
-                     nty, (int)nblk, per_xcd);
+  const int ntx = (w + kTileX - 1) / kTileX;
+  if (cin == 32 && tuning().conv_rolling) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      SFM_HIP(hipFuncSetAttribute((const void*)k_conv3r, hipFuncAttributeMaxDynamicSharedMemorySize, kRLds));
+      attr_set = true;
+    }
+    const int nty = (h + kRTileY - 1) / kRTileY, ndc = (depth + kPlanes - 1) / kPlanes;
+    const int64_t nblk = (int64_t)ntx * nty * ndc * batch;
+    SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
+    const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
+    hipLaunchKernelGGL(k_conv3r, dim3((unsigned)(per_xcd * kXcds)), dim3(256), kRLds, s, (const unsigned short*)in,
+                       (const unsigned short*)weights, scale, bias, (const unsigned short*)residual, relu,
+                       cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w,
+                       ntx, nty, ndc, (int)nblk, per_xcd);
+  } else {
+    const int nty = (h + kTileY - 1) / kTileY;
+    const int64_t nblk = (int64_t)ntx * nty * batch * depth;
+    SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
+    const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
+    hipLaunchKernelGGL(k_conv3, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, (const unsigned short*)in,
+                       cin, (const unsigned short*)weights, scale, bias, (const unsigned short*)residual, relu,
+                       cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w,
+                       ntx, nty, (int)nblk, per_xcd);
+  }
   SFM_LAUNCHED();
   return SFM_OK;
 }

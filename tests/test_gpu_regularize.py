@@ -172,3 +172,25 @@ def test_stack_layers_teacher_forced(cuda):
         if li == 1 or resid:
             keep = y
         x = y
+
+
+@pytest.mark.parametrize("D,h,w", [(13, 9, 70), (8, 4, 64), (2, 5, 3)])
+def test_rolling_kernel_equals_per_plane_kernel(cuda, D, h, w):
+    # k_conv3r (planes staged once, rotating accumulators) adds the same
+    # products in the same order as k_conv3: bit-identical outputs
+    from sfm_amd import _lib
+    from sfm_amd.regularize import conv3_bf16
+    g = torch.Generator().manual_seed(D + h + w)
+    x = torch.randn(1, D, h, w, 32, generator=g).to(torch.bfloat16).to(cuda)
+    wp = (torch.randn(27, 32, 32, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    sc, bi = 0.5 + torch.rand(32, generator=g), 0.1 * torch.randn(32, generator=g)
+    res = torch.randn(1, D, h, w, 32, generator=g).to(torch.bfloat16).to(cuda)
+    outs = []
+    try:
+        for rolling in (0, 1):
+            _lib.tune("conv_rolling", rolling)
+            outs.append((conv3_bf16(x, wp, sc, bi, res, False, 32).cpu(), conv3_bf16(x, wp, sc, bi, None, True, 1).cpu()))
+    finally:
+        _lib.tune("conv_rolling", 1)
+    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16))
+    assert torch.equal(outs[0][1], outs[1][1])
