@@ -17,7 +17,7 @@ average launch durations come from HIP events recorded by libsfm_hip around
 every launch on the launching stream during the timed region; `traffic` is
 the PMC-measured HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950
 correction) from the committed profiles/rNN_pmc.json of the same workload.  The
-`cpu_baseline` is the oracle (CPU restatement) on a bounded sample, rank 0 only.
+`cpu_baseline` is the oracle (CPU restatement) on a bounded sample, rank 0 at N=1 only.
 """
 import argparse
 import json
@@ -223,12 +223,12 @@ def main():
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "inliers": [int(v) for v in inl.cpu()],
         }
-        if not args.no_regularize and hp.cost.dtype in (torch.float32, torch.bfloat16):
+        if world == 1 and not args.no_regularize and hp.cost.dtype in (torch.float32, torch.bfloat16):
             try:
                 out["roofline_regularize"] = regularize_roofline(hp.cost)
             except Exception as e:   # extra information, never the metric
                 out["roofline_regularize"] = {"error": repr(e)}
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
             try:
                 out["cpu_baseline"] = cpu_baseline(flow, K, ref_fea, tgt_fea, P.float(), args)
             except Exception as e:   # the baseline is reported, never the target
