@@ -341,6 +341,72 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
     }
   };
 
+  // Channels-last epilogue through LDS (the staged plane is dead once every
+  // wave has left the MFMA loop): scale/bias/ReLU in the accumulator layout
+  // (lane = pixel, 16 channels), one row at a time into a padded [32 px][36]
+  // fp32 tile per wave, then read back as lane = (pixel, 16 consecutive
+  // channels) so the residual loads and bf16 stores are 32-byte contiguous
+  // per lane and a wave covers its row's 2 KB in one pass.
+  auto store_cl = [&](f32x16* a, int d) {
+    float* T = reinterpret_cast<float*>(lds_in) + wave * (32 * 36);
+    const int px = lane >> 1, half = lane & 1;
+    const int x = x0 + wcol + px;
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      __syncthreads();  // o = 0: every wave is done with the plane; o = 1: row 0's reads are done
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = 8 * q + 4 * h;
+        const float4 sc = *reinterpret_cast<const float4*>(scale + co);
+        const float4 bi = *reinterpret_cast<const float4*>(bias + co);
+        float4 v = make_float4(__builtin_fmaf(a[o][4 * q + 0], sc.x, bi.x), __builtin_fmaf(a[o][4 * q + 1], sc.y, bi.y),
+                               __builtin_fmaf(a[o][4 * q + 2], sc.z, bi.z), __builtin_fmaf(a[o][4 * q + 3], sc.w, bi.w));
+        if (relu) {
+          v.x = fmaxf(v.x, 0.0f);
+          v.y = fmaxf(v.y, 0.0f);
+          v.z = fmaxf(v.z, 0.0f);
+          v.w = fmaxf(v.w, 0.0f);
+        }
+        *reinterpret_cast<float4*>(T + r * 36 + co) = v;
+      }
+      __syncthreads();
+      const int y = y0 + wrow + o;
+      if (y < H && x < W) {
+        const int64_t pix = ((int64_t)b * D + d) * plane + (int64_t)y * W + x;
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float4 t = *reinterpret_cast<const float4*>(T + px * 36 + half * 16 + 4 * k);
+          v[4 * k] = t.x;
+          v[4 * k + 1] = t.y;
+          v[4 * k + 2] = t.z;
+          v[4 * k + 3] = t.w;
+        }
+        if (res) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const uint4 rv = *reinterpret_cast<const uint4*>(res + pix * 32 + half * 16 + 8 * k);
+            const unsigned int w4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[8 * k + 2 * e] += bf2f(w4[e] & 0xffff);
+              v[8 * k + 2 * e + 1] += bf2f(w4[e] >> 16);
+            }
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          uint4 st;
+          st.x = (unsigned)f2bf(v[8 * k + 0]) | ((unsigned)f2bf(v[8 * k + 1]) << 16);
+          st.y = (unsigned)f2bf(v[8 * k + 2]) | ((unsigned)f2bf(v[8 * k + 3]) << 16);
+          st.z = (unsigned)f2bf(v[8 * k + 4]) | ((unsigned)f2bf(v[8 * k + 5]) << 16);
+          st.w = (unsigned)f2bf(v[8 * k + 6]) | ((unsigned)f2bf(v[8 * k + 7]) << 16);
+          *reinterpret_cast<uint4*>(out + pix * 32 + half * 16 + 8 * k) = st;
+        }
+      }
+    }
+  };
+
   // step j stages plane z = d0 - 1 + j and feeds output planes m = j - dz
   // (m in [0, nd)); ring slot of output m is m % 3, i.e. (PH - dz) mod 3.
   const int nsteps = nd + 2;
@@ -403,7 +469,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
       }
     }
     if (v2) {  // output plane m = j - 2 is complete
-      store(acc[(PH + 1) % 3], d0 + j - 2);
+      if (out1) store(acc[(PH + 1) % 3], d0 + j - 2);
+      else store_cl(acc[(PH + 1) % 3], d0 + j - 2);
 #pragma unroll
       for (int o = 0; o < 2; ++o)
         for (int i = 0; i < 16; ++i) acc[(PH + 1) % 3][o][i] = 0.0f;
