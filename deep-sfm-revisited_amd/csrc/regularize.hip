@@ -351,9 +351,13 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
     float* T = reinterpret_cast<float*>(lds_in) + wave * (32 * 36);
     const int px = lane >> 1, half = lane & 1;
     const int x = x0 + wcol + px;
+    __syncthreads();  // every wave is done with the plane (T overlaps other waves' halo rows)
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
-      __syncthreads();  // o = 0: every wave is done with the plane; o = 1: row 0's reads are done
+      // T is private to the wave: LDS ops of one wave complete in order, so
+      // only the compiler must keep row o's writes after row o-1's reads
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int co = 8 * q + 4 * h;
@@ -369,7 +373,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
         }
         *reinterpret_cast<float4*>(T + r * 36 + co) = v;
       }
-      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       const int y = y0 + wrow + o;
       if (y < H && x < W) {
         const int64_t pix = ((int64_t)b * D + d) * plane + (int64_t)y * W + x;
