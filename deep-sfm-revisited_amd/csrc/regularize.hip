@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
 }
 
 // k_conv3r: the cin = 32 layers, rolling along the depth (plane) axis.  A
-// block owns a 4-row x 64-column tile for kPlanes consecutive output planes.
+// block owns a 4-row x 64-column tile for nplanes consecutive output planes (chosen per launch).
 // All 27 weight taps stay resident in LDS (54 KB, staged once per block) and
 // every input plane of the range is staged ONCE (6 x 66 halo, 25 KB): plane
 // z feeds output planes z+1, z and z-1 (dz = 0, 1, 2) from three rotating
@@ -223,7 +223,6 @@ __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
 // cuts the bytes a CU pulls from L2/HBM per MFMA ~3.6x against k_conv3,
 // whose per-CU load rate (~8 B/cycle) was the binding limit (PMC).
 // A wave owns 2 rows x 32 columns: 3 planes x 2 rows = six 32x32 accumulators.
-constexpr int kPlanes = 8;                          // output planes per block
 constexpr int kRTileY = 4;                          // output rows per block
 constexpr int kRHaloY = kRTileY + 2;                // 6
 constexpr int kRInBytes = kRHaloY * kHaloX * 64;    // 25,344
@@ -235,7 +234,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
                                                    const float* __restrict__ scale, const float* __restrict__ bias,
                                                    const unsigned short* __restrict__ res, int relu,
                                                    unsigned short* __restrict__ out, float* __restrict__ out1, int D,
-                                                   int H, int W, int ntx, int nty, int ndc, int nblk, int per_xcd) {
+                                                   int H, int W, int ntx, int nty, int ndc, int nplanes, int nblk,
+                                                   int per_xcd) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   unsigned char* lds_w = lds;
   unsigned char* lds_in = lds + kRWBytes;
@@ -247,8 +247,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
   const int tx = rest % ntx;
   rest /= ntx;
   const int ty = rest % nty, b = rest / nty;
-  const int x0 = tx * kTileX, y0 = ty * kRTileY, d0 = dc * kPlanes;
-  const int nd = min(kPlanes, D - d0);  // output planes of this block
+  const int x0 = tx * kTileX, y0 = ty * kRTileY, d0 = dc * nplanes;
+  const int nd = min(nplanes, D - d0);  // output planes of this block
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -556,14 +556,25 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
       SFM_HIP(hipFuncSetAttribute((const void*)k_conv3r, hipFuncAttributeMaxDynamicSharedMemorySize, kRLds));
       attr_set = true;
     }
-    const int nty = (h + kRTileY - 1) / kRTileY, ndc = (depth + kPlanes - 1) / kPlanes;
+    // Longest plane run that still gives ~one full round of 2 blocks per CU
+    // (fewer halo planes and weight stagings per output plane; measured at
+    // C2: 8 -> 16 -> 32 planes = 748 -> 772 -> 798 TFLOP/s).
+    const int nty = (h + kRTileY - 1) / kRTileY;
+    int nplanes = 4;
+    for (int cand : {32, 16, 8}) {
+      if ((int64_t)ntx * nty * batch * ((depth + cand - 1) / cand) >= 480) {
+        nplanes = cand;
+        break;
+      }
+    }
+    const int ndc = (depth + nplanes - 1) / nplanes;
     const int64_t nblk = (int64_t)ntx * nty * ndc * batch;
     SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
     const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
     hipLaunchKernelGGL(k_conv3r, dim3((unsigned)(per_xcd * kXcds)), dim3(256), kRLds, s, (const unsigned short*)in,
                        (const unsigned short*)weights, scale, bias, (const unsigned short*)residual, relu,
                        cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w,
-                       ntx, nty, ndc, (int)nblk, per_xcd);
+                       ntx, nty, ndc, nplanes, (int)nblk, per_xcd);
   } else {
     const int nty = (h + kTileY - 1) / kTileY;
     const int64_t nblk = (int64_t)ntx * nty * batch * depth;
