@@ -112,3 +112,27 @@ def test_new_entry_points_validate_arguments():
     # tuning knobs: unknown key / out of range
     assert lib.sfm_tune_set(b"no_such_knob", 1) == 1
     assert lib.sfm_tune_set(b"sweep_items_per_block", 3) == 1
+
+
+def test_regularisation_and_flow2depth_validate_arguments():
+    """sfm_conv3_bf16 / sfm_to_channels_last_bf16 / sfm_flow2depth refuse bad
+    shapes before any device work (no GPU here)."""
+    from sfm_amd import _lib
+    lib = _lib.load()
+    v = ctypes.c_void_p(16)
+    o = ctypes.c_void_p(4096)
+    # cin must be 32 or 64, cout 32 or 1, residual only with cout 32
+    assert lib.sfm_conv3_bf16(v, 1, 16, 4, 4, 4, v, v, v, None, 0, 32, o, None) == 1
+    assert b"cin" in lib.sfm_last_error()
+    assert lib.sfm_conv3_bf16(v, 1, 32, 4, 4, 4, v, v, v, None, 0, 8, o, None) == 1
+    assert lib.sfm_conv3_bf16(v, 1, 32, 4, 4, 4, v, v, v, v, 0, 1, o, None) == 1
+    # output aliasing the input, misaligned operands, empty shapes
+    assert lib.sfm_conv3_bf16(v, 1, 32, 4, 4, 4, v, v, v, None, 0, 32, v, None) == 1
+    assert lib.sfm_conv3_bf16(ctypes.c_void_p(18), 1, 32, 4, 4, 4, v, v, v, None, 0, 32, o, None) == 1
+    assert lib.sfm_conv3_bf16(v, 1, 32, 0, 4, 4, v, v, v, None, 0, 32, o, None) == 1
+    # channels-last: dtype code, channel multiple of 8
+    assert lib.sfm_to_channels_last_bf16(v, 2, 1, 64, 100, o, None) == 1
+    assert lib.sfm_to_channels_last_bf16(v, 0, 1, 12, 100, o, None) == 1
+    # flow2depth: empty image
+    assert lib.sfm_flow2depth(v, v, v, 1, 0, 10, o, None) == 1
+    assert lib.sfm_tune_set(b"conv_rolling", 2) == 1
