@@ -72,6 +72,27 @@ class TwoViewHotPath:
         return sweep.plane_sweep_cost(ref_fea, tgt_fea, pose, K4, Ki4, self.L, self.min_depth, self.cost_dtype,
                                       out=self.cost, workspace=self.sweep_ws)
 
+    def step_pipelined(self, flow, K, ref_fea, tgt_fea):
+        """``step`` with the sweep on a side stream: the pose stage runs on
+        the caller's stream and does not wait for the previous step's sweep,
+        so that HBM-bound sweep overlaps the next step's latency-bound
+        five-point solve (1 wave/SIMD).  Same kernels, same results; the
+        sweeps stay ordered on their stream, so the shared cost buffer is
+        written in step order.  The caller synchronises (or waits on
+        ``self.sweep_stream``) before reading the cost volume."""
+        if getattr(self, "sweep_stream", None) is None:
+            self.sweep_stream = torch.cuda.Stream(device=self.device)
+        main = torch.cuda.current_stream(self.device)
+        Kinv = self.k_inverse(K)
+        E, P, inl, win = self.pose(flow, K, Kinv)
+        side = self.sweep_stream
+        side.wait_stream(main)
+        for t in (Kinv, P, K, ref_fea, tgt_fea):
+            t.record_stream(side)       # allocator: live until the side stream is done with them
+        with torch.cuda.stream(side):
+            cost = self.sweep(ref_fea, tgt_fea, P, K, Kinv)
+        return E, P, inl, cost
+
     def step(self, flow, K, ref_fea, tgt_fea):
         Kinv = self.k_inverse(K)
         E, P, inl, win = self.pose(flow, K, Kinv)
