@@ -19,6 +19,8 @@ RTOL, ATOL = 1e-4, 1e-4
     (1, 10, 4, 20, 64, torch.float32, 3),      # slab % 64 == 0, output pointer misaligned
     (1, 5, 3, 11, 19, torch.bfloat16, 1),      # odd slab: bf16 element stores
     (2, 12, 6, 16, 40, torch.bfloat16, 0),     # bf16 pair stores, partial group of 8
+    (1, 8, 4, 9, 13, torch.bfloat16, 2),       # even slab, output 4 B off: pair stores
+    (1, 8, 8, 12, 25, torch.bfloat16, 4),      # even slab, output 8 B off
 ])
 def test_aligned_slab_kernel_matches_per_row(cuda, B, C, L, h, w, dtype, offset):
     from sfm_amd import _lib, synth
