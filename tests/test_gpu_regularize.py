@@ -42,9 +42,11 @@ def _bf16_ulp_close(got, want):
     return int(bad.sum()), float((got - want).abs().max())
 
 
-def test_channels_last_bit_exact(cuda):
+@pytest.mark.parametrize("shape", [(2, 64, 5, 7, 13), (2, 64, 4, 10, 30), (1, 32, 4, 6, 9), (1, 64, 2, 16, 16)])
+def test_channels_last_bit_exact(cuda, shape):
+    # (5, 7, 13): generic kernel; the others (plane % 4 == 0): the float4 kernel
     from sfm_amd.regularize import to_channels_last
-    x = torch.randn(2, 64, 5, 7, 13, generator=torch.Generator().manual_seed(1)) * 10
+    x = torch.randn(*shape, generator=torch.Generator().manual_seed(1)) * 10
     got = to_channels_last(x.to(cuda)).cpu()
     want = x.permute(0, 2, 3, 4, 1).to(torch.bfloat16)
     assert torch.equal(got.view(torch.int16), want.view(torch.int16))
