@@ -588,11 +588,9 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
   ProfScope ps("conv3", s);
   const int ntx = (w + kTileX - 1) / kTileX;
   if (cin == 32 && tuning().conv_rolling) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      SFM_HIP(hipFuncSetAttribute((const void*)k_conv3r, hipFuncAttributeMaxDynamicSharedMemorySize, kRLds));
-      attr_set = true;
-    }
+    // > 64 KB of dynamic LDS must be opted into; set on every launch (cheap,
+    // and correct for whichever device is current and from any host thread)
+    SFM_HIP(hipFuncSetAttribute((const void*)k_conv3r, hipFuncAttributeMaxDynamicSharedMemorySize, kRLds));
     // Longest plane run that still gives ~one full round of 2 blocks per CU
     // (fewer halo planes and weight stagings per output plane; measured at
     // C2: 8 -> 16 -> 32 planes = 748 -> 772 -> 798 TFLOP/s).
