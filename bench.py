@@ -1,37 +1,44 @@
 #!/usr/bin/env python3
 """Benchmark: image-pairs/sec of the two-view SfM hot path on MI355X.
 
-One step = one batch of `--batch` KITTI-shaped pairs (376x1242 dense flow,
-N = 435,032 correspondences) per GPU through
-    flow -> correspondences -> RANSAC five-point (H = 512 x iters = 4096)
+One step = one batch of `--batch` pairs per GPU through
+    flow -> correspondences -> RANSAC five-point (H = 512 x iters)
     -> pose (RESCALE_DEPTH, NORM_TARGET 0.6) -> plane-sweep cost volume
-       [B, 64, 128, 94, 311] fp32
-with every input already resident in HBM (BASELINE.json configs[1]).
-Multi-GPU: one process per GPU (torchrun), pairs shard across ranks with no
-data-path collective ("scaling": "weak"); RCCL only for the barrier and the
-max-over-ranks timing reduction.
+with every input already resident in HBM.  ``--config`` picks the workload
+(BASELINE.json configs):
+
+  c2      (default) 8 KITTI 376x1242 pairs, dense flow N=435,032, H=4096,
+          L=128, fp32 volume [8, 64, 128, 94, 311]        (configs[1])
+  c3      4 KITTI pairs per GPU, bf16 volume: the 8-GPU data-parallel shape
+          (32 pairs on 8 GPUs)                              (configs[2])
+  c4      8 indoor 640x480 pairs, N=285,200, H=2048, L=64 (configs[3])
+  sparse  c2 with the SIFT-keypoint branch of pose_by_ransac: N=2,048
+          keypoints per pair (SFMnet.py:250-254); the solve dominates
+
+Multi-GPU: one process per GPU.  Under torchrun the ranks come from its env;
+``python bench.py --gpus N`` with no WORLD_SIZE starts the N ranks itself
+(fresh child processes, before anything touches the GPU).  Pairs shard
+across ranks with no data-path collective ("scaling": "weak"); RCCL only for
+the barrier, the max-over-ranks timing reduction and the device-name gather.
 
 Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel (RANSAC
-scoring, fp64 VALU); `roofline_sweep` the HBM-bound cost-volume kernel; both
+scoring, fp32 VALU); `roofline_sweep` the HBM-bound cost-volume kernel; both
 average launch durations come from HIP events recorded by libsfm_hip around
 every launch on the launching stream during the timed region; `traffic` is
 the PMC-measured HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950
-correction) from the committed profiles/rNN_pmc.json of the same workload.  The
-`cpu_baseline` is the oracle (CPU restatement) on a bounded sample, rank 0 at N=1 only.
+correction) from the committed profiles/rNN_pmc*.json of the same workload.
+The `cpu_baseline` is the oracle (CPU restatement) on one full pair, rank 0 at
+N=1 only.
 """
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "deep-sfm-revisited_amd"))
-
-import torch  # noqa: E402
-
-from sfm_amd import _lib, dist, ransac, synth  # noqa: E402
-from sfm_amd.pipeline import TwoViewHotPath  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP64_TFLOPS = 78.6      # MI355X fp64 vector spec
@@ -39,73 +46,123 @@ PEAK_FP32_TFLOPS = 157.3     # MI355X fp32 vector spec (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0    # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 FLOP_PER_EVAL = 50           # Ex, xE, x'Ex, sqrt, div, |.|
 
+# name -> (pairs per GPU, image hw, ransac_iter, nlabel, cost dtype, sparse keypoints per pair)
+CONFIGS = {
+    "c2": (8, "kitti", 8, 128, "fp32", 0),
+    "c3": (4, "kitti", 8, 128, "bf16", 0),
+    "c4": (8, "indoor", 4, 64, "fp32", 0),
+    "sparse": (8, "kitti", 8, 128, "fp32", 2048),
+}
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU per step")
-    ap.add_argument("--nlabel", type=int, default=128)
-    ap.add_argument("--iters", type=int, default=8, help="ransac_iter (H = 512 x iters)")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--batch", type=int, default=None, help="pairs per GPU per step (default: the config's)")
+    ap.add_argument("--nlabel", type=int, default=None)
+    ap.add_argument("--iters", type=int, default=None, help="ransac_iter (H = 512 x iters)")
     ap.add_argument("--threshold", type=float, default=1e-4)
-    ap.add_argument("--cost-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--cost-dtype", choices=["fp32", "bf16"], default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-regularize", action="store_true",
                     help="skip the (unscored) PSNet 3-D regularisation roofline line after the timed region")
     ap.add_argument("--fused", action="store_true",
                     help="RANSAC reads the flow directly (sfm_ransac5_flow) instead of materialised correspondences")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-runs", type=int, default=3, help="full-pair CPU baseline runs (median)")
     ap.add_argument("--pipeline", action="store_true",
                     help="sweep on a side stream, overlapping the next step's solve (measured slower: 460 vs 466 pairs/s)")
-    return ap.parse_args()
+    args = ap.parse_args(argv)
+    b, hw, it, nl, cd, kp = CONFIGS[args.config]
+    args.batch = b if args.batch is None else args.batch
+    args.iters = it if args.iters is None else args.iters
+    args.nlabel = nl if args.nlabel is None else args.nlabel
+    args.cost_dtype = cd if args.cost_dtype is None else args.cost_dtype
+    args.hw_name = hw
+    args.keypoints = kp
+    return args
+
+
+def _round_version(path):
+    """profiles/r02_pmc_v10.json -> (2, 10): numeric, so v10 sorts after v6."""
+    m = re.search(r"r(\d+)_pmc(?:_v(\d+))?\.json$", os.path.basename(path))
+    return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, -1)
 
 
 def pmc_traffic(args):
     """HBM bytes per launch of the path's kernels from the newest committed PMC
-    summary (profiles/rNN_pmc.json, scripts/gpu_pmc.sh + scripts/pmc_summary.py;
+    summary (profiles/rNN_pmc[_vK].json, scripts/gpu_pmc.sh + scripts/pmc_summary.py;
     counters need their own profiler pass, so they cannot be read live here).
-    Only reported for the default workload the summary was collected on."""
+    Only reported for the workload the summary was collected on."""
     import glob
-    if (args.batch, args.nlabel, args.iters, args.cost_dtype) != (8, 128, 8, "fp32"):
-        return {}, None
-    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")))
-    if not fs:
-        return {}, None
-    k = json.load(open(fs[-1]))["kernels"]
-    return {n: v.get("hbm_bytes") for n, v in k.items()}, os.path.relpath(fs[-1], ROOT)
+    fs = [f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")) if _round_version(f)[0] >= 0]
+    fs.sort(key=_round_version)
+    for f in reversed(fs):
+        d = json.load(open(f))
+        wl = d.get("workload", {"config": "c2", "batch": 8, "nlabel": 128, "iters": 8, "cost_dtype": "fp32"})
+        if (wl.get("config", "c2"), wl.get("batch"), wl.get("nlabel"), wl.get("iters"), wl.get("cost_dtype")) == \
+                (args.config, args.batch, args.nlabel, args.iters, args.cost_dtype):
+            return {n: v.get("hbm_bytes") for n, v in d["kernels"].items()}, os.path.relpath(f, ROOT)
+    return {}, None
 
 
-def cpu_baseline(flow, K, ref_fea, tgt_fea, pose, args):
-    """Oracle (CPU restatement) on a bounded sample of the same workload:
-    one pair, RANSAC with 64 chains x `iters` (of 512) hypotheses on all
-    435,032 correspondences, and the sweep on 16 of 128 planes; both scaled to
-    one full pair."""
+def cpu_info(threads):
+    import torch
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cores": threads, "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "torch_threads": torch.get_num_threads(), "cpu_model": model}
+
+
+def cpu_baseline(flow, K, ref_fea, tgt_fea, pose, args, n_pts=None, keypoints=None):
+    """Oracle (CPU restatement) on one full pair of the same workload: RANSAC
+    with all 512 chains x `iters` on all N correspondences (C++, OpenMP over
+    chains) and the full L-plane sweep (torch-CPU fp32), after a warm-up; the
+    median of ``--cpu-runs`` runs."""
     import numpy as np
+    import torch
     sys.path.insert(0, ROOT)
     from oracle import ransac5 as ORR
     from oracle import sweep as OSW
+    from sfm_amd import ransac
     threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
     torch.set_num_threads(threads)
     Kinv = torch.inverse(K[:1].cpu())
-    pts = ransac.flow_to_points(flow[:1], Kinv.to(flow.device)).cpu().numpy()[0]
+    if keypoints is None:
+        pts = ransac.flow_to_points(flow[:1], Kinv.to(flow.device)).cpu().numpy()[0]
+    else:
+        pts = ransac.gather_keypoints(flow[:1], Kinv.to(flow.device), keypoints[:1], [n_pts]).cpu().numpy()[0]
     q, qp = np.ascontiguousarray(pts[:, :2]), np.ascontiguousarray(pts[:, 2:])
-    chains = 64
+    r = ref_fea[:1].cpu().float(); t = tgt_fea[:1].cpu().float(); P = pose[:1].cpu(); Kc = K[:1].cpu()
     ORR.ransac5(q[:2000], qp[:2000], iters=1, thr=args.threshold, nchains=8, nthreads=threads)   # warm-up
-    t0 = time.perf_counter()
-    ORR.ransac5(q, qp, iters=args.iters, thr=args.threshold, nchains=chains, nthreads=threads)
-    t_ransac = (time.perf_counter() - t0) * (512 / chains)
-    planes = list(range(0, args.nlabel, max(1, args.nlabel // 16)))
-    r = ref_fea[:1].cpu(); t = tgt_fea[:1].cpu(); P = pose[:1].cpu(); Kc = K[:1].cpu()
-    OSW.plane_sweep_cost(r, t, P, Kc, torch.inverse(Kc), args.nlabel, 1.0, rescale=0.6, planes=planes[:2])
-    t0 = time.perf_counter()
-    OSW.plane_sweep_cost(r, t, P, Kc, torch.inverse(Kc), args.nlabel, 1.0, rescale=0.6, planes=planes)
-    t_sweep = (time.perf_counter() - t0) * (args.nlabel / len(planes))
+    OSW.plane_sweep_cost(r, t, P, Kc, torch.inverse(Kc), args.nlabel, 1.0, rescale=0.6, planes=[0, 1])
+    tr, ts = [], []
+    for _ in range(max(1, args.cpu_runs)):
+        t0 = time.perf_counter()
+        ORR.ransac5(q, qp, iters=args.iters, thr=args.threshold, nchains=512, nthreads=threads)
+        tr.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        OSW.plane_sweep_cost(r, t, P, Kc, torch.inverse(Kc), args.nlabel, 1.0, rescale=0.6)
+        ts.append(time.perf_counter() - t0)
+    t_ransac = float(np.median(tr))
+    t_sweep = float(np.median(ts))
     per_pair = t_ransac + t_sweep
-    return {"value": round(1.0 / per_pair, 4), "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": (f"1 KITTI pair: RANSAC {chains}/512 chains x {args.iters} iters on N=435032 "
-                       f"({t_ransac:.2f} s/pair scaled), sweep {len(planes)}/{args.nlabel} planes "
-                       f"({t_sweep:.3f} s/pair scaled), oracle C++ (OpenMP) + torch-CPU fp32")}
+    out = {"value": round(1.0 / per_pair, 4), "unit": "pairs/s", "kind": "port",
+           "sample": (f"1 full pair, median of {len(tr)} runs after a warm-up: RANSAC 512 chains x {args.iters} "
+                      f"iters on N={q.shape[0]} ({t_ransac:.2f} s, oracle C++ OpenMP), {args.nlabel}-plane sweep "
+                      f"({t_sweep:.3f} s, torch-CPU fp32)")}
+    out.update(cpu_info(threads))
+    return out
 
 
 def regularize_roofline(cost, steps=3):
@@ -113,6 +170,8 @@ def regularize_roofline(cost, steps=3):
     pair of the last step's cost volume, after the timed region.  Not part of
     ``value`` (the metric's path ends at the cost volume); reported so the
     MFMA kernel's roofline is measured live beside the path's."""
+    import torch
+    from sfm_amd import _lib
     from sfm_amd.regularize import CostRegularization
     torch.manual_seed(0)
     reg = CostRegularization(cost.shape[1]).to(cost.device).eval()
@@ -138,22 +197,84 @@ def regularize_roofline(cost, steps=3):
             "note": "not part of value: the CNN after the measured path, timed after it"}
 
 
-def main():
-    args = parse()
+def _stub_mode():
+    """SFM_BENCH_CPU_STUB=1: CPU-only rehearsal of the launch / rank / timing
+    control flow (gloo, a small torch matmul as the step).  Used by
+    tests/test_bench_launch.py; never a measurement."""
+    return os.environ.get("SFM_BENCH_CPU_STUB") == "1"
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.gpus < 1:
+        print("bench: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    from sfm_amd import dist     # torch only: nothing here touches the GPU
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no torchrun: start the N ranks as fresh children and pass on their exit code
+        return dist.launch_local(args.gpus, [sys.executable, os.path.abspath(__file__)] + argv)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world_env}: refusing to report a "
+              f"{world_env}-rank run as {args.gpus}", file=sys.stderr)
+        return 2
+    if _stub_mode():
+        return _main_stub(args, dist)
+    return _main_gpu(args, dist)
+
+
+def _main_stub(args, dist):
+    import torch
+    rank, world, _ = dist.init(backend="gloo")
+    x = torch.randn(64, 64, generator=torch.Generator().manual_seed(rank))
+    for _ in range(args.warmup):
+        x = torch.tanh(x @ x)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = torch.tanh(x @ x)
+    dist.barrier()
+    elapsed = dist.reduce_max(time.perf_counter() - t0)
+    names = dist.device_names(None)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": world * args.batch * args.steps / elapsed, "unit": "pairs/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "dist": {"world_size": torch.distributed.get_world_size() if world > 1 else 1,
+                                   "backend": torch.distributed.get_backend() if world > 1 else None,
+                                   "devices": names},
+                          "config": {"name": args.config, "pairs_per_gpu": args.batch,
+                                     "global_batch": world * args.batch}}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+    return 0
+
+
+def _main_gpu(args, dist):
+    import torch
+    from sfm_amd import _lib, ransac, synth
+    from sfm_amd.pipeline import TwoViewHotPath
     rank, world, local = dist.init()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     B = args.batch
-    hw = synth.KITTI_HW
+    if args.hw_name == "kitti":
+        hw, kcal, hwtxt = synth.KITTI_HW, None, "KITTI 376x1242"
+    else:
+        hw, kcal, hwtxt = synth.INDOOR_HW, synth.INDOOR_K, "indoor 640x480"
     fhw = synth.feature_hw(hw)
     C = 32
     cost_dtype = torch.float32 if args.cost_dtype == "fp32" else torch.bfloat16
 
     # synthetic inputs, distinct pairs per rank, resident in HBM before timing
-    flow, K, pose_gt, _ = synth.kitti_pair_batch(B, seed=1000 + rank, hw=hw, device=dev)
+    flow, K, pose_gt, _ = synth.kitti_pair_batch(B, seed=1000 + rank, hw=hw, device=dev, k=kcal)
     ref_fea, tgt_fea = synth.features(B, C, fhw[0], fhw[1], seed=rank, device=dev)
+    kp = None
+    if args.keypoints:
+        kp = synth.keypoints(B, args.keypoints, hw, seed=rank, device=dev)
     hp = TwoViewHotPath(B, hw, fhw, C, args.nlabel, args.iters, args.threshold, 1.0, rescale_depth=True,
-                        norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused)
+                        norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused,
+                        keypoints=None if kp is None else (kp, [args.keypoints] * B))
 
     # --pipeline: step i's sweep (side stream) overlaps step i+1's five-point solve
     stepf = hp.step_pipelined if args.pipeline else hp.step
@@ -172,14 +293,15 @@ def main():
     elapsed = time.perf_counter() - t0
     _lib.profile_enable(False)
     elapsed = dist.reduce_max(elapsed, dev)
+    names = dist.device_names(dev)
 
     kt = {}
-    for name in ("flow_to_points", "ransac_solve", "ransac_chain", "ransac_score", "ransac_select", "plane_sweep"):
+    for name in ("flow_to_points", "keypoints_to_points", "ransac_solve", "ransac_chain", "ransac_score",
+                 "ransac_select", "plane_sweep"):
         ms, n = _lib.profile_read(name)
-        kt[name] = ms / max(n, 1)
+        if n:
+            kt[name] = ms / n
     cands = ransac.candidate_counts(hp.ws, B, args.iters)
-    if hp.fused:
-        kt.pop("flow_to_points", None)
     evals = sum(cands) * hp.n                       # candidate E x correspondences per launch
     skipped = ransac.skipped_evaluations(hp.ws, B, args.iters)   # exact bound pruning (last launch)
     done = evals - skipped                          # evaluations the launch performed
@@ -189,10 +311,12 @@ def main():
     s = 4 if cost_dtype == torch.float32 else 2
     sweep_bytes = B * (2 * C * args.nlabel * h * w * s + 2 * C * h * w * 4)
     sweep_gbs = sweep_bytes / (kt["plane_sweep"] * 1e-3) / 1e9
+    hyps = B * 512 * args.iters
 
     traffic, traffic_src = pmc_traffic(args)
     if rank == 0:
         pairs = world * B * args.steps
+        corr = (f"{args.keypoints} SIFT-like keypoints" if args.keypoints else f"dense flow (N={hp.n})")
         out = {
             "metric": "image-pairs/sec (5-pt RANSAC + nlabel=128 plane-sweep), KITTI 376x1242",
             "value": round(pairs / elapsed, 3),
@@ -206,12 +330,15 @@ def main():
             "vs_baseline": None,
             "dtype": "f64+" + ("f32" if s == 4 else "bf16"),
             "data": "synthetic (seeded KITTI-shaped rigid scene, 0.5 px noise, 15% outlier flow; N(0,1) features)",
-            "config": {"workload": (f"KITTI 376x1242 dense flow (N={hp.n}), H={512 * args.iters} hypotheses "
-                                    f"(ransac_iter={args.iters}), nlabel={args.nlabel}, C=32 at 94x311, "
-                                    f"{args.cost_dtype} cost volume"),
+            "config": {"name": args.config,
+                       "workload": (f"{hwtxt} {corr}, H={512 * args.iters} hypotheses (ransac_iter={args.iters}), "
+                                    f"nlabel={args.nlabel}, C=32 at {h}x{w}, {args.cost_dtype} cost volume"),
                        "pairs_per_gpu": B, "global_batch": world * B, "parallelism": f"dp{world}",
                        "streams": "sweep on a side stream (overlaps the next step's solve)" if args.pipeline
                        else "one stream"},
+            "dist": {"world_size": torch.distributed.get_world_size() if world > 1 else 1,
+                     "backend": torch.distributed.get_backend() if world > 1 else None,
+                     "devices": names},
             # k_score32 decides ~99% of evaluations in float32 (the rest re-tested in
             # float64), so the binding peak is the float32 VALU one
             "roofline": {"kernel": "ransac_score", "bound": "valu-fp32", "achieved": round(score_tflops, 3),
@@ -226,6 +353,8 @@ def main():
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,
                                "avg_launch_ms": round(kt["plane_sweep"], 4),
                                "bytes_per_launch": sweep_bytes},
+            "solve": {"hypotheses_per_launch": hyps, "ms": round(kt["ransac_solve"], 4),
+                      "hypotheses_per_s": round(hyps / (kt["ransac_solve"] * 1e-3), 1)},
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
             "inliers": [int(v) for v in inl.cpu()],
         }
@@ -236,13 +365,15 @@ def main():
                 out["roofline_regularize"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
             try:
-                out["cpu_baseline"] = cpu_baseline(flow, K, ref_fea, tgt_fea, P.float(), args)
+                out["cpu_baseline"] = cpu_baseline(flow, K, ref_fea, tgt_fea, P.float(), args,
+                                                   n_pts=args.keypoints or None, keypoints=kp)
             except Exception as e:   # the baseline is reported, never the target
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -70,3 +70,53 @@ def barrier(device=None):
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_local(nprocs, argv, env=None):
+    """Start ``nprocs`` ranks of ``argv`` (a command line) on this node, one
+    process per GPU, with the env torchrun would give them (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT).  The caller must not
+    have touched the GPU: the children are fresh processes, never an exec of
+    this one.  Returns the first non-zero exit code (0 if all ranks pass); a
+    failing rank takes the others down."""
+    import subprocess
+    import time
+    port = free_port()
+    procs = []
+    for r in range(int(nprocs)):
+        e = dict(os.environ if env is None else env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_WORLD_SIZE=str(nprocs),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(argv, env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def device_names(device=None):
+    """Per-rank device names, gathered to every rank (rank order)."""
+    import torch
+    name = torch.cuda.get_device_name(device) if device is not None and device.type == "cuda" else "cpu"
+    if not dist.is_initialized():
+        return [name]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, name)
+    return out

@@ -22,7 +22,7 @@ from . import ransac, sweep
 class TwoViewHotPath:
     def __init__(self, batch, image_hw, feat_hw, channels=32, nlabel=128, iters=8, threshold=1e-4,
                  min_depth=1.0, rescale_depth=False, norm_target=0.6, cost_dtype=torch.float32, margin=10,
-                 device="cuda", seed=ransac.DEFAULT_SEED, fused=False):
+                 device="cuda", seed=ransac.DEFAULT_SEED, fused=False, keypoints=None):
         self.batch = int(batch)
         self.H, self.W = image_hw
         self.h, self.w = feat_hw
@@ -38,6 +38,14 @@ class TwoViewHotPath:
         self.n = (self.H - 2 * margin) * (self.W - 2 * margin)
         self.fused = bool(fused)
         B = self.batch
+        # keypoints: (kp [B, n, 2] float32 on the device, counts) -> the sparse
+        # branch of pose_by_ransac (SFMnet.py:250-254) instead of the dense one
+        self.kp = keypoints
+        if keypoints is not None:
+            if self.fused:
+                raise ValueError("the fused flow path is dense-only")
+            self.kp_n = [int(v) for v in keypoints[1]]
+            self.n = max(self.kp_n)
         # fused: RANSAC reads the flow directly (no correspondence buffer)
         self.pts = None if self.fused else torch.empty(B, self.n, 4, dtype=torch.float64, device=self.device)
         self.ws = ransac.workspace_for(B, self.iters, self.device)
@@ -57,8 +65,13 @@ class TwoViewHotPath:
         if self.fused:
             return ransac.ransac5_flow(flow, Kinv, self.iters, self.thr, self.H, self.W, self.margin, seed=self.seed,
                                        workspace=self.ws)
-        ransac.flow_to_points(flow, Kinv, self.H, self.W, self.margin, out=self.pts)
-        E, P, inl, win = ransac.ransac5_batched(self.pts, None, None, None, self.iters, self.thr, self.seed,
+        n = None
+        if self.kp is not None:
+            ransac.gather_keypoints(flow, Kinv, self.kp[0], self.kp_n, "round", out=self.pts)
+            n = self.kp_n
+        else:
+            ransac.flow_to_points(flow, Kinv, self.H, self.W, self.margin, out=self.pts)
+        E, P, inl, win = ransac.ransac5_batched(self.pts, n, None, None, self.iters, self.thr, self.seed,
                                                 True, workspace=self.ws)
         return E, P, inl, win
 

@@ -22,6 +22,29 @@ def _check_dev_f64(t, name):
         raise RuntimeError(f"{name} must be contiguous")
 
 
+def _flow_and_kinv(flow, intrinsic_inv):
+    """Validated float32 flow [B,2,H,W] and per-pair K^-1 [B,3,3] (a shared
+    [3,3] or [1,3,3] K^-1 is broadcast): the kernels read Ki at b*9."""
+    if not flow.is_cuda:
+        raise RuntimeError("flow must be a CUDA tensor")
+    if flow.dim() != 4 or flow.shape[1] != 2:
+        raise RuntimeError(f"flow must be [B,2,H,W], got {tuple(flow.shape)}")
+    B = flow.shape[0]
+    return flow.contiguous().float(), _kinv_batch(intrinsic_inv, B, flow.device)
+
+
+def _kinv_batch(intrinsic_inv, B, device):
+    Ki = intrinsic_inv
+    if Ki.device != device:
+        raise RuntimeError(f"intrinsic_inv must be on {device}, got {Ki.device}")
+    if Ki.dim() == 2:
+        Ki = Ki.unsqueeze(0)
+    if Ki.dim() != 3 or tuple(Ki.shape[1:]) != (3, 3) or Ki.shape[0] not in (1, B):
+        raise RuntimeError(f"intrinsic_inv must be [B,3,3], [1,3,3] or [3,3] with B={B}, got "
+                           f"{tuple(intrinsic_inv.shape)}")
+    return Ki.float().expand(B, 3, 3).contiguous()
+
+
 def hypotheses(iters):
     return CHAINS * int(iters)
 
@@ -125,13 +148,12 @@ def flow_to_points(flow, intrinsic_inv, h_side=None, w_side=None, margin=10, out
     """Dense correspondences of SFMnet.pose_by_ransac (models/SFMnet.py:179-263):
     flow [B,2,H,W] float32, intrinsic_inv [B,3,3] float32 (CUDA) -> pts [B,N,4]
     float64 with N = (h_side-2m)(w_side-2m)."""
-    if not flow.is_cuda:
-        raise RuntimeError("flow must be a CUDA tensor")
-    flow = flow.contiguous().float()
-    Ki = intrinsic_inv.contiguous().float()
+    flow, Ki = _flow_and_kinv(flow, intrinsic_inv)
     B, _, H, W = flow.shape
     h = H if h_side is None else int(h_side)
     w = W if w_side is None else int(w_side)
+    if not (2 * margin < h <= H and 2 * margin < w <= W):
+        raise RuntimeError(f"h_side/w_side ({h}, {w}) must lie in (2*margin, flow size {(H, W)}]")
     N = (h - 2 * margin) * (w - 2 * margin)
     if out is None:
         out = torch.empty(B, N, 4, dtype=torch.float64, device=flow.device)
@@ -179,13 +201,15 @@ def keypoints_to_points(flow, intrinsic_inv, kp1, kp2=None, mode="round", h_side
     if not intrinsic_inv.is_cuda:
         raise RuntimeError("intrinsic_inv must be a CUDA tensor")
     dev = intrinsic_inv.device
-    Ki = intrinsic_inv.contiguous().float()
-    B = Ki.shape[0]
+    B = len(kp1)
+    Ki = _kinv_batch(intrinsic_inv, B, dev)
     if len(kp1) != B or (m == 2 and (kp2 is None or len(kp2) != B)):
         raise RuntimeError("one keypoint array per pair is required")
     if m != 2:
         if not flow.is_cuda:
             raise RuntimeError("flow must be a CUDA tensor")
+        if flow.dim() != 4 or flow.shape[1] != 2 or flow.shape[0] != B:
+            raise RuntimeError(f"flow must be [B,2,H,W] with B={B}, got {tuple(flow.shape)}")
         flow = flow.contiguous().float()
         _, _, H, W = flow.shape
     else:
@@ -212,14 +236,42 @@ def keypoints_to_points(flow, intrinsic_inv, kp1, kp2=None, mode="round", h_side
             a2[b, :n[b]] = np.asarray(kp2[b], dtype=np.float32).reshape(-1, 2)
     t1 = torch.from_numpy(a1).to(dev)
     t2 = torch.from_numpy(a2).to(dev) if m == 2 else None
+    out = gather_keypoints(flow if m != 2 else None, Ki, t1, n, mode, kp2=t2, h_side=h, w_side=w, hw=(H, W),
+                           out=out)
+    return out, n
+
+
+def gather_keypoints(flow, intrinsic_inv, kp1, n, mode="round", kp2=None, h_side=None, w_side=None, hw=None,
+                     out=None):
+    """Device-resident form of ``keypoints_to_points``: kp1 (and kp2 for
+    "sift_pose") are [B, n_max, 2] float32 CUDA tensors already prepared as
+    that function does (rounded and wrapped for "round"); ``n`` the per-pair
+    counts.  One launch, no host copies (the bench's sparse step)."""
+    m = KEYPOINT_MODES[mode]
+    B, nmax, _ = kp1.shape
+    dev = kp1.device
+    Ki = _kinv_batch(intrinsic_inv, B, dev)
+    if m != 2:
+        if flow is None or flow.dim() != 4 or flow.shape[:2] != (B, 2):
+            raise RuntimeError("flow [B,2,H,W] is required for this keypoint mode")
+        flow = flow.contiguous().float()
+        H, W = flow.shape[2:]
+    else:
+        if kp2 is None or tuple(kp2.shape) != tuple(kp1.shape):
+            raise RuntimeError("SIFT_POSE needs target keypoints of the same shape as kp1")
+        H, W = hw if hw is not None else (int(h_side or 1), int(w_side or 1))
+    h = H if h_side is None else int(h_side)
+    w = W if w_side is None else int(w_side)
+    if len(n) != B:
+        raise RuntimeError("one keypoint count per pair is required")
     if out is None:
-        out = torch.zeros(B, nmax, 4, dtype=torch.float64, device=dev)
+        out = torch.zeros(B, max(nmax, 1), 4, dtype=torch.float64, device=dev)
     with torch.cuda.device(dev):
         _lib.check(_lib.load().sfm_keypoints_to_points(
-            None if m == 2 else _lib.ptr(flow), B, H, W, h, w, _lib.ptr(t1), None if t2 is None else _lib.ptr(t2),
-            nmax, _lib.i64_array(n), m, _lib.ptr(Ki), _lib.ptr(out), out.shape[1], _lib.stream_ptr(dev)),
-            "sfm_keypoints_to_points")
-    return out, n
+            None if m == 2 else _lib.ptr(flow), B, H, W, h, w, _lib.ptr(kp1.contiguous()),
+            None if kp2 is None else _lib.ptr(kp2.contiguous()), nmax, _lib.i64_array(n), m, _lib.ptr(Ki),
+            _lib.ptr(out), out.shape[1], _lib.stream_ptr(dev)), "sfm_keypoints_to_points")
+    return out
 
 
 def optimise_batched(pts, E_init, delta=0.001, alpha=0.0, max_reps=200, n=None, workspace=None):
@@ -250,13 +302,12 @@ def ransac5_flow(flow, intrinsic_inv, iters=5, threshold=1e-4, h_side=None, w_si
     """Fused dense path (SFMnet.py:179-274 without the correspondence buffer):
     RANSAC straight from flow [B,2,H,W] float32 and K^-1 [B,3,3] (CUDA).
     Bit-identical to ransac5_batched(flow_to_points(flow, K^-1), ...)."""
-    if not flow.is_cuda:
-        raise RuntimeError("flow must be a CUDA tensor")
-    flow = flow.contiguous().float()
-    Ki = intrinsic_inv.contiguous().float()
+    flow, Ki = _flow_and_kinv(flow, intrinsic_inv)
     B, _, H, W = flow.shape
     h = H if h_side is None else int(h_side)
     w = W if w_side is None else int(w_side)
+    if not (2 * margin < h <= H and 2 * margin < w <= W):
+        raise RuntimeError(f"h_side/w_side ({h}, {w}) must lie in (2*margin, flow size {(H, W)}]")
     dev = flow.device
     Hh = hypotheses(iters)
     with torch.cuda.device(dev):

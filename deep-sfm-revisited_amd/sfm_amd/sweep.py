@@ -20,6 +20,19 @@ def _dev_f32(t, name):
     return t.contiguous().float()
 
 
+def _refuse_grad(**tensors):
+    """The sweep kernels are forward-only: they return tensors with no autograd
+    link.  The reference backpropagates through grid_sample into the target
+    features (models/PSNet.py:155), so a grad-requiring input would silently
+    lose its gradient here -- refuse it instead."""
+    if not torch.is_grad_enabled():
+        return
+    for name, t in tensors.items():
+        if t is not None and t.requires_grad:
+            raise RuntimeError(f"{name} requires grad, but the HIP plane sweep is forward-only (no backward "
+                               f"kernel); run it under torch.no_grad() or detach the input")
+
+
 def check_sizes(t, name, expected):
     """models/inverse_warp.py:19-24"""
     ok = t.dim() == len(expected) and all(
@@ -40,6 +53,8 @@ def plane_sweep_cost(ref_fea, tgt_fea, pose, intrinsics4, intrinsics_inv4, nlabe
     resolution.  ``dtype``: torch.float32 or torch.bfloat16.  Planes are
     d_i = MIN_DEPTH*L/(i+1), or (i+1)*MIN_DEPTH with ``predict_by_depth``
     (cfg.PREDICT_BY_DEPTH, PSNet.py:150-153)."""
+    _refuse_grad(ref_fea=None if warped_only else ref_fea, tgt_fea=tgt_fea, pose=pose,
+                 intrinsics4=intrinsics4, intrinsics_inv4=intrinsics_inv4)
     tgt = _dev_f32(tgt_fea, "tgt_fea")
     B, C, h, w = tgt.shape
     ref = None if warped_only else _dev_f32(ref_fea, "ref_fea")
@@ -78,15 +93,22 @@ def inverse_warp(feat, depth, pose, intrinsics, intrinsics_inv, padding_mode="ze
     assert intrinsics_inv.size() == intrinsics.size()
     if padding_mode != "zeros":
         raise NotImplementedError("only padding_mode='zeros' is on the plane-sweep path")
+    _refuse_grad(feat=feat, depth=depth, pose=pose, intrinsics=intrinsics, intrinsics_inv=intrinsics_inv)
     f = _dev_f32(feat, "feat")
     B, C, h, w = f.shape
+    if tuple(depth.shape) != (B, h, w) or pose.size(0) != B or intrinsics.size(0) != B:
+        raise RuntimeError(f"inverse_warp: depth {tuple(depth.shape)}, pose {tuple(pose.shape)} and intrinsics "
+                           f"{tuple(intrinsics.shape)} must match feat {(B, C, h, w)}")
+    # every converted operand is bound to a local until the launch is enqueued:
+    # a temporary freed inside the call could be handed to the next copy
     d = _dev_f32(depth, "depth")
+    pose32 = _dev_f32(pose, "pose")
+    K32 = _dev_f32(intrinsics, "intrinsics")
+    Ki32 = _dev_f32(intrinsics_inv, "intrinsics_inv")
     out = torch.empty_like(f)
     with torch.cuda.device(f.device):
-        rc = _lib.load().sfm_inverse_warp(_lib.ptr(f), B, C, h, w, _lib.ptr(d), _lib.ptr(_dev_f32(pose, "pose")),
-                                          _lib.ptr(_dev_f32(intrinsics, "intrinsics")),
-                                          _lib.ptr(_dev_f32(intrinsics_inv, "intrinsics_inv")), _lib.ptr(out),
-                                          _lib.stream_ptr(f.device))
+        rc = _lib.load().sfm_inverse_warp(_lib.ptr(f), B, C, h, w, _lib.ptr(d), _lib.ptr(pose32), _lib.ptr(K32),
+                                          _lib.ptr(Ki32), _lib.ptr(out), _lib.stream_ptr(f.device))
         _lib.check(rc, "sfm_inverse_warp")
     return out
 

@@ -100,3 +100,14 @@ def feature_hw(hw=KITTI_HW):
     """Feature-map size after the two stride-2 convs of PSNet's feature CNN (submodule.py:112,120)."""
     h, w = hw
     return ((h + 1) // 2 + 1) // 2, ((w + 1) // 2 + 1) // 2   # 376x1242 -> 94x311
+
+
+def keypoints(batch, n, hw=KITTI_HW, margin=10, seed=0, device="cpu"):
+    """Sparse (SIFT-like) keypoints for the bench's sparse regime (SURVEY.md
+    §8(d): N=2,048 random pixels per pair): [B, n, 2] float32 (x, y) pixel
+    positions, already rounded to integers as SFMnet.py:250-253 does."""
+    gen = torch.Generator().manual_seed(int(seed) + 104729)
+    H, W = hw
+    x = torch.randint(margin, W - margin, (batch, n), generator=gen)
+    y = torch.randint(margin, H - margin, (batch, n), generator=gen)
+    return torch.stack([x, y], -1).float().to(device)

@@ -1,0 +1,59 @@
+"""bench.py's multi-rank control flow on CPU (gloo): `python bench.py --gpus N`
+without torchrun starts N ranks itself, every rank runs the same timed loop,
+the max over ranks is reported and the JSON line carries the world size the
+process group saw.  The HIP step is replaced by a CPU stub
+(SFM_BENCH_CPU_STUB=1) -- only the launch / rank / timing path is exercised."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None, timeout=180):
+    env = dict(os.environ, SFM_BENCH_CPU_STUB="1", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def _json_line(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_spawns_two_ranks_without_torchrun():
+    r = _run(["--gpus", "2", "--steps", "3", "--warmup", "1", "--config", "c3"])
+    assert r.returncode == 0, r.stderr
+    out = _json_line(r.stdout)
+    assert out["n_gpus"] == 2
+    assert out["dist"]["world_size"] == 2 and out["dist"]["backend"] == "gloo"
+    assert out["dist"]["devices"] == ["cpu", "cpu"]
+    assert out["config"]["pairs_per_gpu"] == 4 and out["config"]["global_batch"] == 8
+
+
+def test_single_rank_default():
+    r = _run(["--steps", "2", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr
+    out = _json_line(r.stdout)
+    assert out["n_gpus"] == 1 and out["dist"]["world_size"] == 1
+    assert out["config"]["name"] == "c2" and out["config"]["pairs_per_gpu"] == 8
+
+
+def test_gpus_and_world_size_mismatch_fails():
+    r = _run(["--gpus", "2", "--steps", "1"], extra_env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_pmc_summaries_sort_numerically():
+    sys.path.insert(0, ROOT)
+    import bench
+    fs = ["profiles/r01_pmc_v6.json", "profiles/r01_pmc_v10.json", "profiles/r02_pmc.json", "profiles/r01_pmc.json"]
+    assert sorted(fs, key=bench._round_version) == ["profiles/r01_pmc.json", "profiles/r01_pmc_v6.json",
+                                                   "profiles/r01_pmc_v10.json", "profiles/r02_pmc.json"]
