@@ -11,6 +11,16 @@ Run in the survey container, where /root/reference exists:
   /root/reference/models/inverse_warp.py and models/flow2depth.py on the CPU
   (their `.cuda()` calls are made no-ops for the duration of the call).
   The PSNet loop around inverse_warp (PSNet.py:144-157) is restated here.
+* corr.npz: the reference's own SFMnet.pose_by_ransac (models/SFMnet.py:
+  176-274, flow2coord 298-318, epipolar_utils.compute_P_matrix_ransac) run on
+  the CPU with cv2 / essential_matrix / the flow and pose networks replaced by
+  stand-ins (_RefEnv); the stand-in computeP records the float64
+  correspondences the reference hands to the extension.  Dense, rounded
+  keypoint, SAMPLE_SP and SIFT_POSE branches.
+* psnet.npz (SURVEY §8(c) golden #5): the reference PSNet (models/PSNet.py,
+  submodule.py) at seed 0 on a reduced 128x192 pair, nlabel 16, eval mode with
+  seeded BatchNorm3d statistics; forward hooks record the features, the cost
+  volume, the classify output and the soft-argmin depth (depth_init).
 
 Only inputs and outputs are written (no reference source).
 """
@@ -217,6 +227,222 @@ def gen_warp(rng):
     return out
 
 
+class _Obj:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class _RefEnv:
+    """sys.modules stand-ins for what the reference imports but this container
+    lacks (easydict, path, cv2, the essential_matrix extension) or what the
+    path under test does not use (flow / pose networks, models/__init__.py).
+    Restores sys.modules, sys.path and Tensor.cuda / Module.cuda on exit."""
+
+    def __init__(self):
+        import sys
+        import types
+        self.sys, self.types = sys, types
+        self.captured = []
+
+    def __enter__(self):
+        import pathlib
+        import sys
+        types = self.types
+        self.saved_modules = dict(sys.modules)
+        self.saved_path = list(sys.path)
+        self.orig_tcuda, self.orig_mcuda = torch.Tensor.cuda, torch.nn.Module.cuda
+        torch.Tensor.cuda = lambda t, *a, **k: t
+        torch.nn.Module.cuda = lambda m, *a, **k: m
+
+        class EasyDict(dict):
+            def __getattr__(self, k):
+                try:
+                    return self[k]
+                except KeyError as e:
+                    raise AttributeError(k) from e
+
+            def __setattr__(self, k, v):
+                self[k] = v
+        ed = types.ModuleType("easydict"); ed.EasyDict = EasyDict
+        pa = types.ModuleType("path"); pa.Path = pathlib.Path
+        env = self
+
+        def computeP(q, qp, num_test, num_ransac_test, iters, thr):
+            env.captured.append(dict(q=q.detach().clone(), qp=qp.detach().clone(), num_test=num_test,
+                                     num_ransac_test=num_ransac_test, iters=iters, thr=thr))
+            return torch.eye(3, dtype=torch.float64), torch.zeros(3, 4, dtype=torch.float64), 0
+        em = types.ModuleType("essential_matrix"); em.computeP = computeP
+        em.initialise = lambda *a: torch.eye(3, dtype=torch.float64)
+        em.optimise = lambda *a: torch.eye(3, dtype=torch.float64)
+        cv = types.ModuleType("cv2")
+        cv.xfeatures2d = _Obj(SIFT_create=lambda: None, SURF_create=lambda: None)
+        cv.FlannBasedMatcher = lambda *a, **k: None
+        models = types.ModuleType("models"); models.__path__ = [os.path.join(REF, "models")]
+        models.DICL_shallow = object
+        raft = types.ModuleType("models.RAFT.core.raft"); raft.RAFT = object
+        pose = types.ModuleType("models.PoseNet")
+        pose.ResNet = pose.Bottleneck = pose.PlainPose = object
+        sys.modules.update({"easydict": ed, "path": pa, "essential_matrix": em, "cv2": cv, "models": models,
+                            "models.RAFT": types.ModuleType("models.RAFT"),
+                            "models.RAFT.core": types.ModuleType("models.RAFT.core"),
+                            "models.RAFT.core.raft": raft, "models.PoseNet": pose})
+        sys.path.insert(0, REF)
+        return self
+
+    def import_(self, name):
+        import importlib
+        return importlib.import_module(name)
+
+    def __exit__(self, *a):
+        import sys
+        for k in list(sys.modules):
+            if k not in self.saved_modules:
+                del sys.modules[k]
+        sys.modules.update(self.saved_modules)
+        sys.path[:] = self.saved_path
+        torch.Tensor.cuda, torch.nn.Module.cuda = self.orig_tcuda, self.orig_mcuda
+
+
+class _KP:
+    def __init__(self, x, y):
+        self.pt = (float(x), float(y))
+
+
+class _Match:
+    def __init__(self, q, t, d):
+        self.queryIdx, self.trainIdx, self.distance = q, t, d
+
+
+def gen_corr():
+    """Reference correspondence build (SFMnet.pose_by_ransac) -> the float64
+    q / qp the reference passes to essential_matrix.computeP."""
+    g = torch.Generator().manual_seed(11)
+    B, H, W = 2, 48, 70
+    flow = (torch.rand(B, 2, H, W, generator=g) - 0.5) * 40.0
+    K = torch.tensor([[[60.0, 0, 34.5], [0, 58.0, 23.5], [0, 0, 1]],
+                      [[72.5, 0, 35.25], [0, 71.0, 24.1], [0, 0, 1]]])
+    Kinv = torch.inverse(K)
+    img = torch.zeros(B, 3, H, W)
+    nkp = 40
+    kp1 = torch.stack([torch.rand(B, nkp, generator=g) * (W - 1.0), torch.rand(B, nkp, generator=g) * (H - 1.0)], -1)
+    kp2 = kp1 + (torch.rand(B, nkp, 2, generator=g) - 0.5) * 6.0
+    out = {}
+    with _RefEnv() as env:
+        SF = env.import_("models.SFMnet")
+        cfg = env.import_("lib.config").cfg
+
+        def net(matches):
+            m = SF.SFMnet.__new__(SF.SFMnet)
+            torch.nn.Module.__init__(m)
+            m.delta, m.alpha, m.maxreps = 0.001, 0.0, 200
+            m.min_matches, m.ransac_iter, m.ransac_threshold = 20, 5, 1e-4
+            calls = {"n": 0}
+
+            def detect(img_u8, mask):
+                b = calls["n"] // 2
+                which = calls["n"] % 2
+                calls["n"] += 1
+                if not matches:
+                    return [], None
+                pts = (kp1 if which == 0 else kp2)[b]
+                return [_KP(x, y) for x, y in pts.tolist()], np.zeros((nkp, 8), np.float32)
+            m.sift = _Obj(detectAndCompute=detect)
+            m.surf = _Obj(detectAndCompute=detect)
+
+            def knn(d1, d2, k=2):
+                if not matches:
+                    raise RuntimeError("no descriptors")
+                return [(_Match(i, i, 1.0), _Match(i, (i + 1) % nkp, 2.0)) for i in range(nkp)]
+            m.flann = _Obj(knnMatch=knn)
+            return m
+
+        cases = [("dense", False, dict(SIFT_POSE=False, SAMPLE_SP=False), None),
+                 ("dense_side", False, dict(SIFT_POSE=False, SAMPLE_SP=False), (40, 64)),
+                 ("round", True, dict(SIFT_POSE=False, SAMPLE_SP=False), None),
+                 ("sample_sp", True, dict(SIFT_POSE=False, SAMPLE_SP=True), None),
+                 ("sift_pose", True, dict(SIFT_POSE=True, SAMPLE_SP=False), None)]
+        for name, matches, flags, side in cases:
+            saved = {k: cfg[k] for k in flags}
+            cfg.update(flags)
+            env.captured.clear()
+            m = net(matches)
+            hs, ws = (None, None) if side is None else side
+            f = flow if side is None else flow[:, :, :side[0], :side[1]].contiguous()
+            m.pose_by_ransac(f, img, img, Kinv, hs, ws)
+            cfg.update(saved)
+            out[name] = dict(q=np.stack([c["q"].numpy() for c in env.captured]),
+                             qp=np.stack([c["qp"].numpy() for c in env.captured]),
+                             num_test=np.array([c["num_test"] for c in env.captured]),
+                             iters=np.array([c["iters"] for c in env.captured]))
+        # epipolar_utils glue around the extension (epipolar_utils.py:87-135) with
+        # stand-in solver outputs: records the casts and F = K^-T E K^-1
+        EU = env.import_("epipolar_utils")
+        em = env.import_("essential_matrix")
+        E_fix = torch.randn(3, 3, generator=g, dtype=torch.float64)
+        P_fix = torch.randn(3, 4, generator=g, dtype=torch.float64)
+        em.computeP = lambda q, qp, a, b, c, d: (E_fix.clone(), P_fix.clone(), 17)
+        em.initialise = lambda q, qp, a, b, c, d: E_fix.clone()
+        c1 = torch.from_numpy(out["dense"]["q"][0]).float()
+        c2 = torch.from_numpy(out["dense"]["qp"][0]).float()
+        Eo, Po, Fo, n_in = EU.compute_P_matrix_ransac(c1, c2, Kinv[0], 0.001, 0.0, 200, len(c1), len(c1), 5, 1e-4)
+        Ee, Fe = EU.compute_E_matrix_ransac(c1, c2, Kinv[0], 0.001, 0.0, 200, len(c1), len(c1), 5, 1e-4)
+        out["epipolar"] = dict(E_stub=E_fix.numpy(), P_stub=P_fix.numpy(), Kinv=Kinv[0].numpy(),
+                               P_E=Eo.numpy(), P_P=Po.numpy(), P_F=Fo.numpy(), P_inliers=np.int32(n_in),
+                               E_E=Ee.numpy(), E_F=Fe.numpy())
+    out["input"] = dict(flow=flow.numpy(), K=K.numpy(), Kinv=Kinv.numpy(), kp1=kp1.numpy(), kp2=kp2.numpy(),
+                        side=np.array([40, 64]))
+    return out
+
+
+def gen_psnet():
+    """SURVEY §8(c) golden #5: reference PSNet depth at seed 0, reduced size."""
+    B, H, W, L = 1, 128, 192, 16
+    out = {}
+    with _RefEnv() as env:
+        cfg = env.import_("lib.config").cfg
+        cfg.update(PSNET_CONTEXT=False, RESCALE_DEPTH=True, NORM_TARGET=0.8)
+        PS = env.import_("models.PSNet")
+        torch.manual_seed(0)
+        net = PS.PSNet(L, 1.0)
+        g = torch.Generator().manual_seed(5)
+        for mod in net.modules():        # checkpoint-like BatchNorm3d state (exercises the folding)
+            if isinstance(mod, torch.nn.BatchNorm3d):
+                c = mod.num_features
+                mod.running_mean.copy_(0.1 * torch.randn(c, generator=g))
+                mod.running_var.copy_(0.5 + torch.rand(c, generator=g))
+                mod.weight.data.copy_(0.8 + 0.4 * torch.rand(c, generator=g))
+                mod.bias.data.copy_(0.1 * torch.randn(c, generator=g))
+        net.eval()
+        rec = {"fea": []}
+        net.feature_extraction.register_forward_hook(lambda m, i, o: rec["fea"].append(o.detach().clone()))
+        net.dres0.register_forward_pre_hook(lambda m, i: rec.__setitem__("cost", i[0].detach().clone()))
+        net.classify.register_forward_hook(lambda m, i, o: rec.__setitem__("classify", o.detach().clone()))
+        ref = torch.rand(B, 3, H, W, generator=g) * 2 - 1
+        tgt = torch.rand(B, 3, H, W, generator=g) * 2 - 1
+        K = torch.tensor([[[100.0, 0, 95.5], [0, 98.0, 63.5], [0, 0, 1]]])
+        Kinv = torch.inverse(K)
+        a = torch.tensor([[0, -0.02, 0.01], [0.02, 0, -0.015], [-0.01, 0.015, 0.0]])
+        pose = torch.cat([torch.matrix_exp(a), torch.tensor([[0.2], [-0.05], [-1.2]])], 1).reshape(1, 1, 3, 4)
+        pose_in = pose.clone()
+        with torch.no_grad():
+            net(ref, [tgt], pose.clone(), K, Kinv)
+            # random-init features reach ~1e8 logits (no trained BN statistics):
+            # scale the last Conv3d so the logits have std 4, the regime of a
+            # trained net whose softmax over planes is not one-hot
+            net.classify[2].weight.mul_(4.0 / float(rec["classify"].std()))
+            rec["fea"].clear()
+            depth_init, depth = net(ref, [tgt], pose_in, K, Kinv)
+        state = {k: v.numpy() for k, v in net.state_dict().items()
+                 if k.startswith("dres") or k.startswith("classify")}
+    out["input"] = dict(ref_img=ref.numpy(), tgt_img=tgt.numpy(), K=K.numpy(), Kinv=Kinv.numpy(),
+                        pose=pose.numpy(), pose_rescaled=pose_in.numpy(), nlabel=np.int32(L),
+                        min_depth=np.float32(1.0), norm_target=np.float32(0.8))
+    out["out"] = dict(ref_fea=rec["fea"][0].numpy(), tgt_fea=rec["fea"][1].numpy(), cost=rec["cost"].numpy(),
+                      classify=rec["classify"].numpy(), depth_init=depth_init.numpy(), depth=depth.numpy())
+    out["state"] = state
+    return out
+
+
 def _save(name, d):
     flat = {}
     for k, v in d.items():
@@ -230,14 +456,27 @@ def _save(name, d):
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
-def main():
+def main(argv=None):
+    """python -m oracle.gen_golden [name ...]  (default: every fixture)."""
+    import sys
+    want = set((sys.argv[1:] if argv is None else argv) or
+               ["solve5", "ransac", "irls", "sampler", "warp", "corr", "psnet"])
     os.makedirs(OUT, exist_ok=True)
     rng = np.random.default_rng(20241015)
-    _save("solve5.npz", gen_solve5(rng))
-    _save("ransac.npz", gen_ransac(rng))
-    _save("irls.npz", gen_irls(rng))
-    _save("sampler.npz", gen_sampler())
-    _save("warp.npz", gen_warp(rng))
+    # the rng is consumed in this order, so a subset regenerates identical files
+    for name, fn in (("solve5", gen_solve5), ("ransac", gen_ransac), ("irls", gen_irls)):
+        d = fn(rng)
+        if name in want:
+            _save(name + ".npz", d)
+    if "sampler" in want:
+        _save("sampler.npz", gen_sampler())
+    d = gen_warp(rng)
+    if "warp" in want:
+        _save("warp.npz", d)
+    if "corr" in want:
+        _save("corr.npz", gen_corr())
+    if "psnet" in want:
+        _save("psnet.npz", gen_psnet())
 
 
 if __name__ == "__main__":

@@ -136,6 +136,24 @@ def test_full_size_dense_pair(cuda):
     assert abs(abs(np.dot(t, tg / np.linalg.norm(tg))) - 1.0) < 5e-2
 
 
+def test_full_size_kitti_h4096_vs_oracle(cuda):
+    """C2 at full size: one KITTI pair, N = 435,032, H = 4096 (ransac_iter 8).
+    The default launch (exact bound pruning on) and the per-hypothesis-score
+    launch (pruning off) both give the oracle's winner, count, E and P; the
+    latter also every hypothesis score."""
+    from sfm_amd import ransac, synth
+    flow, K, pose, depth = synth.kitti_pair_batch(1, seed=21)
+    pts = ransac.flow_to_points(flow.to(cuda), torch.inverse(K).to(cuda))
+    E, P, inl, win = ransac.ransac5_batched(pts, None, None, None, 8, 1e-4)
+    E2, P2, inl2, win2, scores = ransac.ransac5_batched(pts, None, None, None, 8, 1e-4, return_scores=True)
+    p = pts[0].cpu().numpy()
+    ref = R.ransac5(p[:, :2], p[:, 2:], 435032, 435032, 8, 1e-4, nthreads=16)
+    for e, pp, i, w in ((E, P, inl, win), (E2, P2, inl2, win2)):
+        assert int(w[0]) == ref["winner"] and int(i[0]) == ref["inliers"]
+        assert np.array_equal(e[0].cpu().numpy(), ref["E"]) and np.array_equal(pp[0].cpu().numpy(), ref["P"])
+    assert np.array_equal(scores[0].cpu().numpy(), ref["hyp_score"])
+
+
 @pytest.mark.parametrize("thr,scale", [(1e-4, 1.0), (1e-2, 1.0), (3e-6, 1.0), (1e-3, 1e3), (1e-3, 1e-3)])
 def test_fast_path_guard_near_epipole(cuda, thr, scale):
     """Forward motion puts the epipole in the image: half of the points are

@@ -119,3 +119,25 @@ def test_flow2depth_oracle(golden):
     out = S.flow2depth(torch.from_numpy(g["R"]), torch.from_numpy(g["T"]), torch.zeros(*g["shape"].tolist()),
                        torch.from_numpy(g["K"]))
     assert torch.allclose(out, torch.from_numpy(g["out"]), rtol=0, atol=1e-5)
+
+
+MODES = ("round", "sample_sp", "sift_pose")
+
+
+def test_flow_oracle_matches_reference_correspondences(golden):
+    """oracle/flow.py vs the float64 correspondences the reference's own
+    SFMnet.pose_by_ransac hands to essential_matrix.computeP (corr.npz, made by
+    oracle/gen_golden.py:gen_corr): bit-identical in every branch."""
+    from oracle import flow as OF
+    g = golden("corr.npz")
+    inp = g["input"]
+    flow, Ki = inp["flow"], inp["Kinv"]
+    for name, side in (("dense", None), ("dense_side", inp["side"])):
+        f = flow if side is None else np.ascontiguousarray(flow[:, :, :side[0], :side[1]])
+        q, qp = OF.dense_correspondences(f, Ki)
+        assert np.array_equal(q, g[name]["q"]) and np.array_equal(qp, g[name]["qp"]), name
+        assert list(g[name]["num_test"]) == [q.shape[1]] * 2           # SFMnet.py:269: N for both counts
+    for mode in MODES:
+        for b in range(flow.shape[0]):
+            q, qp = OF.keypoint_correspondences(flow[b], Ki[b], inp["kp1"][b], inp["kp2"][b], mode=mode)
+            assert np.array_equal(q, g[mode]["q"][b]) and np.array_equal(qp, g[mode]["qp"][b]), (mode, b)

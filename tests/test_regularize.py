@@ -1,6 +1,7 @@
 """CPU checks of the PSNet cost-regularisation mirror (no compute on a GPU):
 module layout matches PSNet.py:79-102, the folded layer plan reproduces the
 modules' own forward, and the product path refuses CPU tensors."""
+import numpy as np
 import pytest
 import torch
 
@@ -61,3 +62,35 @@ def test_product_path_refuses_cpu_tensors():
     m = _module(1)
     with pytest.raises(RuntimeError):
         m(torch.randn(1, 64, 3, 4, 5))
+
+
+def _psnet_module(g):
+    from sfm_amd.regularize import CostRegularization
+    m = CostRegularization(64)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in g["state"].items()})
+    return m.eval()
+
+
+def test_oracles_match_reference_psnet(golden):
+    """psnet.npz (SURVEY §8(c) golden #5, the reference PSNet's own forward at
+    seed 0): the sweep oracle rebuilds its cost volume from its features, the
+    regularisation oracle its classify output, the head oracle its depth."""
+    from oracle import regularize as R
+    from oracle import sweep as S
+    g = golden("psnet.npz")
+    inp, out = g["input"], g["out"]
+    L = int(inp["nlabel"])
+    K = torch.from_numpy(inp["K"]); Ki = torch.from_numpy(inp["Kinv"])
+    pose = torch.from_numpy(inp["pose_rescaled"])[:, 0]
+    cost = S.plane_sweep_cost(torch.from_numpy(out["ref_fea"]), torch.from_numpy(out["tgt_fea"]), pose, K, Ki, L,
+                              float(inp["min_depth"]))
+    want = torch.from_numpy(out["cost"])
+    assert float((cost - want).abs().max()) <= 1e-5
+    m = _psnet_module(g)
+    cls = R.regularize_fp32_plan(m, want)          # folded-BN plan == the reference's module forward
+    ref_cls = torch.from_numpy(out["classify"])
+    assert float((cls - ref_cls).abs().max()) <= 1e-4 * float(ref_cls.abs().max())
+    depth = S.depth_head(ref_cls, L, float(inp["min_depth"]), out_hw=tuple(inp["ref_img"].shape[2:]))
+    assert float(((depth - torch.from_numpy(out["depth_init"])).abs() / depth.abs()).max()) <= 1e-6
+    # PSNET_CONTEXT off: the refined depth equals depth_init
+    assert np.array_equal(out["depth"], out["depth_init"])
