@@ -99,6 +99,7 @@ int sfm_tune_set(const char* key, int value) {
   else if (k == "score_mfma" && (value == 0 || value == 1)) t.score_mfma = value;
   else if (k == "score_interleave" && (value == 0 || value == 1)) t.score_interleave = value;
   else if (k == "conv_rolling" && (value == 0 || value == 1)) t.conv_rolling = value;
+  else if (k == "score_precision" && (value == 64 || value == 32 || value == 16)) t.score_precision = value;
   else { sfm::set_error("sfm_tune_set: unknown key or value out of range: " + k); return SFM_ERR_ARG; }
   return SFM_OK;
 }

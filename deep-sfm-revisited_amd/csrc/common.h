@@ -22,6 +22,8 @@ struct Tuning {
   int score_prune = 1;           // exact bound pruning in k_score32 (PruneState)
   int score_mfma = 0;            // 1: k_score_mx, linear forms on the matrix cores (measured 2.3x slower)
   int score_interleave = 0;      // k_score32 items: pairs interleaved (1) or pair after pair (0)
+  int score_precision = 64;      // 64: exact (reference float64 decisions); 32 / 16: ComputeError<float> /
+                                 // <half> semantics (approximate inlier sets, BASELINE C5)
   int conv_rolling = 1;          // 1: cin-32 conv layers roll along the planes (k_conv3r); 0: k_conv3
 };
 Tuning& tuning();

@@ -561,6 +561,57 @@ __device__ __forceinline__ bool inlier_test(const double* E, const Addends& ad, 
   return in;
 }
 
+// Reduced-precision scoring (tuning key score_precision; BASELINE C5's fp32 vs
+// fp16 inlier-set sweep).  ComputeError<T> (kernel_functions.cu:232-264) with
+// the Ematrix, q and qp held in T: every operation of the reference's
+// expression tree rounded to T (RNE, source order, no contraction), sqrt and
+// division correctly rounded in T, and the reference call site's test
+// `error <= c_inlier_threshold` against the float64 threshold
+// (kernel_functions.cu:193-194).  E is first scaled by a power of two (exact;
+// the error is invariant to the scale of E).  Inputs reach T through float32
+// (float64 -> float32 -> T), as the conversion hardware does.  For T = half the sqrt and
+// the division run in float32 and round once to half: float32 carries
+// 24 >= 2*11 + 2 bits, so that double rounding is exact (the result is the
+// correctly rounded half).  oracle/ransac5_oracle.cpp:is_inlier_lp restates it.
+template <int PREC>
+struct LowP { using T = float; };
+template <>
+struct LowP<16> { using T = _Float16; };
+
+template <int PREC>
+__device__ __forceinline__ bool inlier_lowp(const double* E, double xd, double yd, double xpd, double ypd,
+                                            double thr) {
+  using T = typename LowP<PREC>::T;
+  // E scaled by a power of two to max |E_ij| in [0.5, 1): exact in float64,
+  // and the Sampson error is invariant to the scale of E; without it a
+  // five-point E of small norm underflows in half
+  double m = 0.0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m = fmax(m, fabs(E[i]));
+  int ex = 0;
+  if (m > 0.0 && m < 0x1p1000) (void)frexp(m, &ex);
+  T e[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) e[i] = (T)(float)ldexp(E[i], -ex);
+  const T x = (T)(float)xd, y = (T)(float)yd, xp = (T)(float)xpd, yp = (T)(float)ypd;
+  // every intermediate is a named T: assignment rounds each operation to T
+  T m0, m1, s;
+  m0 = e[0] * x; m1 = e[1] * y; s = m0 + m1; const T ex0 = s + e[2];
+  m0 = e[3] * x; m1 = e[4] * y; s = m0 + m1; const T ex1 = s + e[5];
+  m0 = e[6] * x; m1 = e[7] * y; s = m0 + m1; const T ex2 = s + e[8];
+  m0 = xp * e[0]; m1 = yp * e[3]; s = m0 + m1; const T xe0 = s + e[6];
+  m0 = xp * e[1]; m1 = yp * e[4]; s = m0 + m1; const T xe1 = s + e[7];
+  m0 = xp * ex0; m1 = yp * ex1; s = m0 + m1; const T a = s + ex2;
+  T D;
+  m0 = ex0 * ex0; m1 = ex1 * ex1; D = m0 + m1;
+  m0 = xe0 * xe0; D = D + m0;
+  m0 = xe1 * xe1; D = D + m0;
+  const T d = (T)sqrtf((float)D);
+  T err = (T)((float)a / (float)d);
+  if (err < (T)0.0f) err = -err;
+  return (double)(float)err <= thr;
+}
+
 // Level-3 test (reference order), kept as a named call site for the drain.
 __device__ __forceinline__
 bool inlier_reference_call(const double* E, double x, double y, double xp, double yp,
@@ -571,7 +622,7 @@ bool inlier_reference_call(const double* E, double x, double y, double xp, doubl
 // One chunk (kPPL points per lane) against the tile's nc candidates.  One
 // ballot per (candidate, point); the num_test / num_ransac_test prefixes are
 // applied as precomputed wave masks (SAME: both prefixes equal, one count).
-template <bool FAST, bool UNITM, bool SAME>
+template <bool FAST, bool UNITM, bool SAME, int PREC>
 __device__ __forceinline__ void score_chunk(const double* __restrict__ CE, int nc, const double (&x)[kPPL],
                                             const double (&y)[kPPL], const double (&xp)[kPPL],
                                             const double (&yp)[kPPL], const double (&mm2)[kPPL],
@@ -587,7 +638,9 @@ __device__ __forceinline__ void score_chunk(const double* __restrict__ CE, int n
     int sT = 0, sR = 0;
 #pragma unroll
     for (int k = 0; k < kPPL; ++k) {
-      const uint64_t m = __ballot(inlier_test<FAST, UNITM>(E, ad, Kg, x[k], y[k], xp[k], yp[k], mm2[k], kc));
+      const bool in = PREC == 64 ? inlier_test<FAST, UNITM>(E, ad, Kg, x[k], y[k], xp[k], yp[k], mm2[k], kc)
+                                 : inlier_lowp<PREC>(E, x[k], y[k], xp[k], yp[k], kc.thr);
+      const uint64_t m = __ballot(in);
       sT += __popcll(m & mT[k]);
       if (!SAME) sR += __popcll(m & mR[k]);
     }
@@ -599,7 +652,7 @@ __device__ __forceinline__ void score_chunk(const double* __restrict__ CE, int n
   }
 }
 
-template <bool FAST, class Src>
+template <bool FAST, class Src, int PREC = 64>
 __global__ __launch_bounds__(kScoreThreads) void k_score(const Src src, PairParams pp, int batch, int cmax,
                                                          const int32_t* __restrict__ cand_total,
                                                          const double* __restrict__ candE,
@@ -653,11 +706,11 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const Src src, PairPara
       }
       const bool all_unit = __all(unit);
       if (T == R) {
-        if (all_unit) score_chunk<FAST, true, true>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
-        else score_chunk<FAST, false, true>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
+        if (all_unit) score_chunk<FAST, true, true, PREC>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
+        else score_chunk<FAST, false, true, PREC>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
       } else {
-        if (all_unit) score_chunk<FAST, true, false>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
-        else score_chunk<FAST, false, false>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
+        if (all_unit) score_chunk<FAST, true, false, PREC>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
+        else score_chunk<FAST, false, false, PREC>(CE, nc, x, y, xp, yp, mm2, mT, mR, kc, lane, s_cnt[wv]);
       }
     }
     __syncthreads();
@@ -1518,7 +1571,9 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                        w.ncand, w.hypE, w.hypP);
   }
   SFM_LAUNCHED();
-  const bool fast = thr >= 0x1p-40 && thr < 1.0;
+  const int prec = tuning().score_precision;
+  // reduced precision: no exactness guards; the plain ComputeError<T> kernel
+  const bool fast = prec == 64 && thr >= 0x1p-40 && thr < 1.0;
   const double guard_g = fast ? 0x1p24 * (11.0 + 11.0 / thr) : 0.0;
   const bool fast32 = fast && thr >= 0x1p-20 && tuning().score_fp32;
   {
@@ -1553,7 +1608,13 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   }
   {
     ProfScope ps("ransac_score", s);
-    if (fast32 && same && tuning().score_mfma)
+    if (prec == 32)
+      hipLaunchKernelGGL((k_score<false, Src, 32>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
+                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
+    else if (prec == 16)
+      hipLaunchKernelGGL((k_score<false, Src, 16>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
+                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
+    else if (fast32 && same && tuning().score_mfma)
       hipLaunchKernelGGL(k_score_mx<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.cntT, w.cntR, kc);
     else if (fast32)

@@ -81,11 +81,36 @@ def ransac5(q, qp, num_test_points, num_ransac_test_points, iters, threshold, se
     return E, P, inl, win
 
 
+class score_precision:
+    """Context manager selecting the inlier-scoring precision of the RANSAC
+    calls inside it (tuning key "score_precision", process-wide): 64 (the
+    default) reproduces the reference's float64 decisions exactly; 32 / 16
+    evaluate ComputeError<float> / <half> (approximate inlier sets; BASELINE
+    C5's fp32-vs-fp16 sweep).  Not thread-safe across concurrent callers."""
+
+    def __init__(self, bits):
+        if int(bits) not in (64, 32, 16):
+            raise ValueError("score precision must be 64, 32 or 16")
+        self.bits = int(bits)
+
+    def __enter__(self):
+        _lib.tune("score_precision", self.bits)
+        return self
+
+    def __exit__(self, *exc):
+        _lib.tune("score_precision", 64)
+
+
 def ransac5_batched(pts, n=None, num_test_points=None, num_ransac_test_points=None, iters=5, threshold=1e-4,
-                    seed=DEFAULT_SEED, cheirality=True, return_scores=False, workspace=None):
+                    seed=DEFAULT_SEED, cheirality=True, return_scores=False, workspace=None, precision=64):
     """Batched pairs on packed correspondences pts [B, Nstride, 4] float64
     (x, y, x', y').  ``n``: points per pair (default: all Nstride).  Returns
-    (E [B,3,3], P [B,3,4] or None, inliers [B] int32, winner [B] int32[, scores [B,H]])."""
+    (E [B,3,3], P [B,3,4] or None, inliers [B] int32, winner [B] int32[, scores [B,H]]).
+    ``precision``: inlier-scoring precision (see ``score_precision``)."""
+    if int(precision) != 64:
+        with score_precision(precision):
+            return ransac5_batched(pts, n, num_test_points, num_ransac_test_points, iters, threshold, seed,
+                                   cheirality, return_scores, workspace)
     _check_dev_f64(pts, "pts")
     if pts.dim() != 3 or pts.shape[2] != 4:
         raise RuntimeError("pts must be [B, N, 4]")

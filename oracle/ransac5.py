@@ -57,6 +57,12 @@ def lib():
                                      ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                      _dp, _dp, _ip, _ip, _ip, _ip, _ip]
         _lib.orc_ransac5.restype = ctypes.c_int
+        _lib.orc_ransac5_prec.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_double, ctypes.c_uint64, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, _dp, _dp, _ip, _ip, _ip, _ip, _ip]
+        _lib.orc_ransac5_prec.restype = ctypes.c_int
+        _lib.orc_inlier_mask_prec.argtypes = [_dp, _dp, _dp, ctypes.c_int64, ctypes.c_double, ctypes.c_int, _u8p]
+        _lib.orc_inlier_mask_prec.restype = None
         _lib.orc_inlier_mask.argtypes = [_dp, _dp, _dp, ctypes.c_int64, ctypes.c_double, _u8p]
         _lib.orc_inlier_mask.restype = None
         _lib.orc_sample_index.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int64]
@@ -113,9 +119,10 @@ def philox_u32(seed, h, d):
 
 
 def ransac5(q, qp, num_test=None, num_ransac_test=None, iters=5, thr=1e-4, seed=1234, cheir=True,
-            nchains=512, nthreads=0, use_ref=False):
+            nchains=512, nthreads=0, use_ref=False, prec=64):
     """Full RANSAC emulation for one pair. Returns dict(E, P, inliers, winner,
-    hyp_score, hyp_ncand)."""
+    hyp_score, hyp_ncand).  prec: 64 (the reference's ComputeError<double>),
+    32 / 16 (ComputeError<float> / <half>, ransac5_oracle.cpp:is_inlier_lp)."""
     q = np.ascontiguousarray(q, dtype=np.float64)
     qp = np.ascontiguousarray(qp, dtype=np.float64)
     n = q.shape[0]
@@ -131,22 +138,50 @@ def ransac5(q, qp, num_test=None, num_ransac_test=None, iters=5, thr=1e-4, seed=
                                int(cheir), _ptr(E), _ptr(P), ctypes.byref(inl), ctypes.byref(win),
                                _ptr(score, _ip), _ptr(ncand, _ip))
     else:
-        rc = lib().orc_ransac5(_ptr(q), _ptr(qp), n, num_test, num_ransac_test, nchains, iters, thr, seed,
-                               int(cheir), nthreads, _ptr(E), _ptr(P), ctypes.byref(inl), ctypes.byref(win),
-                               _ptr(score, _ip), _ptr(ncand, _ip), _ptr(best, _ip))
+        rc = lib().orc_ransac5_prec(_ptr(q), _ptr(qp), n, num_test, num_ransac_test, nchains, iters, thr, seed,
+                                    int(cheir), nthreads, int(prec), _ptr(E), _ptr(P), ctypes.byref(inl),
+                                    ctypes.byref(win), _ptr(score, _ip), _ptr(ncand, _ip), _ptr(best, _ip))
     if rc != 0:
         raise RuntimeError("oracle ransac5: invalid arguments")
     return dict(E=E.reshape(3, 3), P=P.reshape(3, 4), inliers=inl.value, winner=win.value,
                 hyp_score=score, hyp_ncand=ncand, hyp_best=best)
 
 
-def inlier_mask(E, q, qp, thr):
+def inlier_mask(E, q, qp, thr, prec=64):
     E = np.ascontiguousarray(E, dtype=np.float64).reshape(9)
     q = np.ascontiguousarray(q, dtype=np.float64)
     qp = np.ascontiguousarray(qp, dtype=np.float64)
     m = np.zeros(q.shape[0], dtype=np.uint8)
-    lib().orc_inlier_mask(_ptr(E), _ptr(q), _ptr(qp), q.shape[0], thr, _ptr(m, _u8p))
+    if prec == 64:
+        lib().orc_inlier_mask(_ptr(E), _ptr(q), _ptr(qp), q.shape[0], thr, _ptr(m, _u8p))
+    else:
+        lib().orc_inlier_mask_prec(_ptr(E), _ptr(q), _ptr(qp), q.shape[0], thr, int(prec), _ptr(m, _u8p))
     return m.astype(bool)
+
+
+def inlier_mask_numpy(E, q, qp, thr, prec):
+    """numpy restatement of ransac5_oracle.cpp:is_inlier_lp (checks the C++
+    half rounding): numpy float16 / float32 arithmetic rounds every operation
+    to the type; float16 ops are computed in float32 and rounded once, which
+    is the correctly rounded half result (24 >= 2*11 + 2 bits)."""
+    T = np.float16 if prec == 16 else np.float32
+    c = lambda v: np.asarray(np.asarray(v, np.float64).astype(np.float32)).astype(T)
+    E = np.asarray(E, np.float64).reshape(9)
+    m = float(np.abs(E).max())
+    ex = int(np.frexp(m)[1]) if 0.0 < m < 2.0 ** 1000 else 0
+    e = c(np.ldexp(E, -ex))                 # exact power-of-two scaling to max |E_ij| in [0.5, 1)
+    x, y, xp, yp = c(q[:, 0]), c(q[:, 1]), c(qp[:, 0]), c(qp[:, 1])
+    with np.errstate(all="ignore"):
+        ex0 = (e[0] * x + e[1] * y) + e[2]
+        ex1 = (e[3] * x + e[4] * y) + e[5]
+        ex2 = (e[6] * x + e[7] * y) + e[8]
+        xe0 = (xp * e[0] + yp * e[3]) + e[6]
+        xe1 = (xp * e[1] + yp * e[4]) + e[7]
+        a = (xp * ex0 + yp * ex1) + ex2
+        D = ((ex0 * ex0 + ex1 * ex1) + xe0 * xe0) + xe1 * xe1
+        d = np.sqrt(D.astype(np.float32)).astype(T)
+        err = np.abs((a.astype(np.float32) / d.astype(np.float32)).astype(T))
+    return err.astype(np.float64) <= thr
 
 
 def _decomp(L, prefix, E):

@@ -637,9 +637,68 @@ static inline bool is_inlier(const double* E, double x, double y, double xp, dou
   return e <= thr;
 }
 
-static int64_t count_inliers(const double* E, const double* q, const double* qp, int64_t n, double thr) {
+// Round a float to the nearest binary16 value (ties to even; subnormals;
+// overflow to inf), returned as a float.  x / q and nearbyintf are exact /
+// round-to-nearest-even for the power-of-two quantum q.
+static inline float h16(float f) {
+  if (!std::isfinite(f)) return f;
+  const float a = std::fabs(f);
+  if (a >= 65520.0f) return std::copysign(INFINITY, f);     // past max (65504) + half an ulp
+  float q;
+  if (a < 0x1p-14f) {
+    q = 0x1p-24f;                                            // subnormal quantum
+  } else {
+    int e;
+    std::frexp(a, &e);                                       // a in [2^(e-1), 2^e)
+    q = std::ldexp(1.0f, e - 1 - 10);
+  }
+  return std::copysign(std::nearbyint(a / q) * q, f);
+}
+
+// ComputeError<T> (kernel_functions.cu:232-264) with E, q, qp held in T
+// (T = float for prec 32, binary16 for prec 16), E first scaled by a power of
+// two to max |E_ij| in [0.5, 1) (exact; the error is invariant to the scale of
+// E, and a small-norm five-point E would underflow in half); every operation rounded to T
+// in the reference's source order; sqrt and division correctly rounded (for
+// half computed in float and rounded once: 24 >= 2*11+2 bits makes the double
+// rounding exact, as for + - *); inputs reach T through float32; the count
+// test against the float64 threshold as at kernel_functions.cu:193-194.
+// Mirrors ransac5.hip:inlier_lowp.
+template <int PREC>
+static inline bool is_inlier_lp(const double* E, double xd, double yd, double xpd, double ypd, double thr) {
+  auto r = [](float v) { return PREC == 16 ? h16(v) : v; };
+  double m = 0.0;
+  for (int i = 0; i < 9; ++i) m = std::fmax(m, std::fabs(E[i]));
+  int ex = 0;
+  if (m > 0.0 && m < 0x1p1000) (void)std::frexp(m, &ex);     // max |E_ij| * 2^-ex in [0.5, 1): exact scaling
+  float e[9];
+  for (int i = 0; i < 9; ++i) e[i] = r((float)std::ldexp(E[i], -ex));
+  const float x = r((float)xd), y = r((float)yd), xp = r((float)xpd), yp = r((float)ypd);
+  auto mul = [&](float a, float b) { return r(a * b); };
+  auto add = [&](float a, float b) { return r(a + b); };
+  const float ex0 = add(add(mul(e[0], x), mul(e[1], y)), e[2]);
+  const float ex1 = add(add(mul(e[3], x), mul(e[4], y)), e[5]);
+  const float ex2 = add(add(mul(e[6], x), mul(e[7], y)), e[8]);
+  const float xe0 = add(add(mul(xp, e[0]), mul(yp, e[3])), e[6]);
+  const float xe1 = add(add(mul(xp, e[1]), mul(yp, e[4])), e[7]);
+  const float a = add(add(mul(xp, ex0), mul(yp, ex1)), ex2);
+  const float D = add(add(add(mul(ex0, ex0), mul(ex1, ex1)), mul(xe0, xe0)), mul(xe1, xe1));
+  const float d = r(std::sqrt(D));
+  float err = r(a / d);
+  if (err < 0.0f) err = -err;
+  return (double)err <= thr;
+}
+
+static inline bool is_inlier_p(const double* E, double x, double y, double xp, double yp, double thr, int prec) {
+  if (prec == 32) return is_inlier_lp<32>(E, x, y, xp, yp, thr);
+  if (prec == 16) return is_inlier_lp<16>(E, x, y, xp, yp, thr);
+  return is_inlier(E, x, y, xp, yp, thr);
+}
+
+static int64_t count_inliers(const double* E, const double* q, const double* qp, int64_t n, double thr,
+                             int prec = 64) {
   int64_t c = 0;
-  for (int64_t k = 0; k < n; ++k) c += is_inlier(E, q[2 * k], q[2 * k + 1], qp[2 * k], qp[2 * k + 1], thr);
+  for (int64_t k = 0; k < n; ++k) c += is_inlier_p(E, q[2 * k], q[2 * k + 1], qp[2 * k], qp[2 * k + 1], thr, prec);
   return c;
 }
 
@@ -686,6 +745,12 @@ void orc_inlier_mask(const double* E, const double* q, const double* qp, int64_t
   for (int64_t k = 0; k < n; ++k) mask[k] = is_inlier(E, q[2 * k], q[2 * k + 1], qp[2 * k], qp[2 * k + 1], thr);
 }
 
+void orc_inlier_mask_prec(const double* E, const double* q, const double* qp, int64_t n, double thr, int prec,
+                          uint8_t* mask) {
+  for (int64_t k = 0; k < n; ++k)
+    mask[k] = is_inlier_p(E, q[2 * k], q[2 * k + 1], qp[2 * k], qp[2 * k + 1], thr, prec);
+}
+
 // Full RANSAC over one pair, restating EstimateProjectionMatrix<5> /
 // EstimateEssentialMatrix<5> (kernel_functions.cu:53-226) for `nchains`
 // chains x `iters` iterations (reference: 512 threads), plus the host argmax
@@ -696,10 +761,12 @@ void orc_inlier_mask(const double* E, const double* q, const double* qp, int64_t
 //   * if no hypothesis has > 0 inliers, E = P = 0, inliers = 0, winner = -1.
 // hyp_score (optional, nchains*iters): rescored inlier count per hypothesis.
 // hyp_ncand (optional): nP (cheir) / nroots (no cheir) per hypothesis.
-int orc_ransac5(const double* q, const double* qp, int64_t n, int num_test, int num_ransac_test,
-                int nchains, int iters, double thr, uint64_t seed, int cheir, int nthreads,
-                double* E_out, double* P_out, int* inliers_out, int* winner_out,
-                int* hyp_score, int* hyp_ncand, int* hyp_best) {
+// prec: 64 = ComputeError<double> (the reference), 32 / 16 = is_inlier_lp.
+int orc_ransac5_prec(const double* q, const double* qp, int64_t n, int num_test, int num_ransac_test,
+                     int nchains, int iters, double thr, uint64_t seed, int cheir, int nthreads, int prec,
+                     double* E_out, double* P_out, int* inliers_out, int* winner_out,
+                     int* hyp_score, int* hyp_ncand, int* hyp_best) {
+  if (prec != 64 && prec != 32 && prec != 16) return 1;
   if (n < 1 || num_test < 0 || num_ransac_test < 0 || num_test > n || num_ransac_test > n) return 1;
   const int H = nchains * iters;
   std::vector<int> score(H, 0), best(H, 0);
@@ -730,11 +797,11 @@ int orc_ransac5(const double* q, const double* qp, int64_t n, int num_test, int 
       ncand[h] = nc;
       int bi = 0, bc = 0;
       for (int j = 0; j < nc; ++j) {
-        int c = (int)count_inliers(Es[j], q, qp, num_test, thr);
+        int c = (int)count_inliers(Es[j], q, qp, num_test, thr, prec);
         if (c > bc) { bc = c; bi = j; }
       }
       best[h] = bi;
-      score[h] = (int)count_inliers(Es[bi], q, qp, num_ransac_test, thr);
+      score[h] = (int)count_inliers(Es[bi], q, qp, num_ransac_test, thr, prec);
       memcpy(&Ewin[(size_t)h * 9], Es[bi], sizeof(double) * 9);
       memcpy(&Pwin[(size_t)h * 12], Ps[bi], sizeof(double) * 12);
       memcpy(Eslots, Es, sizeof(Es));
@@ -763,6 +830,14 @@ int orc_ransac5(const double* q, const double* qp, int64_t n, int num_test, int 
   if (hyp_ncand) memcpy(hyp_ncand, ncand.data(), sizeof(int) * H);
   if (hyp_best) memcpy(hyp_best, best.data(), sizeof(int) * H);
   return 0;
+}
+
+int orc_ransac5(const double* q, const double* qp, int64_t n, int num_test, int num_ransac_test,
+                int nchains, int iters, double thr, uint64_t seed, int cheir, int nthreads,
+                double* E_out, double* P_out, int* inliers_out, int* winner_out,
+                int* hyp_score, int* hyp_ncand, int* hyp_best) {
+  return orc_ransac5_prec(q, qp, n, num_test, num_ransac_test, nchains, iters, thr, seed, cheir, nthreads, 64,
+                          E_out, P_out, inliers_out, winner_out, hyp_score, hyp_ncand, hyp_best);
 }
 
 // ---------------------------------------------------------------------------

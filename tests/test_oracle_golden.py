@@ -141,3 +141,20 @@ def test_flow_oracle_matches_reference_correspondences(golden):
         for b in range(flow.shape[0]):
             q, qp = OF.keypoint_correspondences(flow[b], Ki[b], inp["kp1"][b], inp["kp2"][b], mode=mode)
             assert np.array_equal(q, g[mode]["q"][b]) and np.array_equal(qp, g[mode]["qp"][b]), (mode, b)
+
+
+@pytest.mark.parametrize("prec", [32, 16])
+def test_lowp_inlier_oracle_matches_numpy(prec):
+    """ransac5_oracle.cpp:is_inlier_lp (software half rounding h16) vs numpy's
+    own float16 / float32 arithmetic, on geometric and random E of very
+    different scales (the power-of-two normalisation) and thresholds."""
+    from oracle.gen_golden import geometric_scene
+    rng = np.random.default_rng(prec)
+    q, qp = geometric_scene(rng, 4000, out_frac=0.3, noise=0.003)
+    r = R.ransac5(q, qp, iters=1, thr=1e-3, nchains=32)
+    Es = [r["E"], r["E"] * 1e-7, r["E"] * 3e6] + [rng.normal(size=(3, 3)) * s for s in (1e-9, 1.0, 1e9)]
+    for E in Es:
+        for thr in (1e-4, 1e-3, 1e-2, 0.5):
+            a = R.inlier_mask(E, q, qp, thr, prec)
+            b = R.inlier_mask_numpy(E, q, qp, thr, prec)
+            assert np.array_equal(a, b), (thr, int((a != b).sum()))
