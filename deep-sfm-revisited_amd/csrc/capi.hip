@@ -97,6 +97,8 @@ int sfm_tune_set(const char* key, int value) {
   else if (k == "score_fp32" && (value == 0 || value == 1)) t.score_fp32 = value;
   else if (k == "score_prune" && (value == 0 || value == 1)) t.score_prune = value;
   else if (k == "score_mfma" && (value == 0 || value == 1)) t.score_mfma = value;
+  else if (k == "score_mf" && (value == 0 || value == 1)) t.score_mf = value;
+  else if (k == "score_mf_blocks_per_cu" && value >= 1 && value <= 8) t.score_mf_blocks_per_cu = value;
   else if (k == "score_interleave" && (value == 0 || value == 1)) t.score_interleave = value;
   else if (k == "conv_rolling" && (value == 0 || value == 1)) t.conv_rolling = value;
   else if (k == "score_precision" && (value == 64 || value == 32 || value == 16)) t.score_precision = value;

@@ -64,6 +64,7 @@ struct Workspace {
   int32_t* cntT;       // [B][Cmax]
   int32_t* cntR;       // [B][Cmax]
   int32_t* score;      // [B][H]
+  _Float16* candF;     // [B][Cmax][64] split-f16 A rows of k_score_mf (k_mf_cands)
   unsigned long long* cov;      // [B][Cmax] pruning bound state: count | points covered << 32
   int32_t* best_lb;             // [64] largest partial count seen (a lower bound on the winning score)
   unsigned long long* skipped;  // [1] evaluations skipped by pruning (whole call)
@@ -93,6 +94,7 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   t.best_lb = (int32_t*)take(SFM_MAX_BATCH * 64 * 4);    // kBestStride
   t.skipped = (unsigned long long*)take(8);
   t.score = (int32_t*)take(bc * H * 4);
+  t.candF = (_Float16*)take(bc * C * 64 * 2);
   t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
   if (w) *w = t;
   return off;
@@ -1544,6 +1546,8 @@ __global__ void k_keypoint_points(const float* __restrict__ flow, int H, int W, 
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
+#include "score_mf.h"
+
 template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
@@ -1598,7 +1602,9 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   // exact bound pruning: SFMnet's num_test == num_ransac_test, no per-hypothesis scores requested
   bool same = true;
   for (int b = 0; b < bc; ++b) same = same && pp.test[b] == pp.rtest[b];
-  kc.prune = (fast32 && same && !score_out && tuning().score_prune) ? 1 : 0;
+  MfParams mp{};
+  const bool use_mf = fast32 && tuning().score_mf && !tuning().score_mfma && mf_params(thr, &mp);
+  kc.prune = (fast32 && !use_mf && same && !score_out && tuning().score_prune) ? 1 : 0;
   kc.ws_batch = ws_batch;
   kc.interleave = tuning().score_interleave;
   SFM_REQUIRE(prune_state(w.cntR, ws_batch, cmax).skipped == w.skipped, "internal: pruning state layout");
@@ -1608,7 +1614,17 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   }
   {
     ProfScope ps("ransac_score", s);
-    if (prec == 32)
+    if (use_mf) {
+      hipLaunchKernelGGL(k_mf_cands, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax, w.cand_total, w.candE,
+                         w.candF, mp);
+      const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
+      if (same)
+        hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
+                           w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
+      else
+        hipLaunchKernelGGL((k_score_mf<Src, false>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
+                           w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
+    } else if (prec == 32)
       hipLaunchKernelGGL((k_score<false, Src, 32>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.cntT, w.cntR, kc);
     else if (prec == 16)

@@ -1,0 +1,572 @@
+// Phase 3d of the RANSAC (included by ransac5.hip): inlier scoring on the
+// matrix cores with split-f16 operands (k_score_mf, the default scorer).
+//
+// The Sampson test of ComputeError (kernel_functions.cu:232-264) is, per
+// (candidate E, point), a comparison of two polynomials in the point:
+//   a = x'^T E x          bilinear: 9 monomials (x'x, x'y, x', y'x, y'y, y', x, y, 1)
+//   D = |Ex|_01^2 + |x'^T E|_01^2   quadratic: 11 monomials (x^2, y^2, 1, xy, x, y,
+//                                   x'^2, y'^2, x'y', x', y')
+// inlier iff a^2 <= thr^2 D.  For a tile of 32 candidates x 32 points both are
+// 32x32 GEMMs over the monomials, K <= 16: v_mfma_f32_32x32x16_f16 tiles.
+//
+//   a  needs ~22 significant bits (it cancels from terms ~1 down to ~1e-4):
+//      coefficients c and monomials m are split c = c_hi + c_lo (f16 each) and
+//      a = sum c_hi m_hi + c_hi m_lo + c_lo m_hi: 27 products, two MFMAs
+//      (hi x hi first, from a zero accumulator).
+//   D  has no such cancellation away from the epipole: one f16 MFMA each for
+//      Ylo ~ t_lo D - eps_in and Yhi ~ t_hi D + eps_out, the two sides of the
+//      decision band; eps and every error bound enter through two extra
+//      monomials M^2, M^4 (M = max(1, |x|, |y|, |x'|, |y'|)).
+// Decision per output element (3 VALU): aa = a*a; inlier iff aa < Ylo,
+// outlier iff aa > Yhi; otherwise undecided -> the wave's LDS queue -> the
+// float64 test of k_score32 (inlier_f64v + reference order).
+//
+// Error bounds (u = 2^-24; everything scaled: a' = 2^k a with 2^k <= 1/thr,
+// E pre-scaled by a power of two to max |E_ij| in [0.5, 1); S = sum |c_j m_j|
+// <= |c|_1 M^2):
+//   * split representation: |c - c_hi - c_lo| <= 2^-22 |c| (+2^-25 absolute
+//     when c_lo is subnormal), same for m; the dropped c_lo m_lo <= 2^-22 |c m|
+//     -> 3 * 2^-22 S + 18 * 2^-25 (max|c| + M^2); the monomials are formed in
+//     float32 from float32 coordinates, +0.75 * 2^-22 S (3.75 * 2^-22 in all).
+//   * MFMA accumulation: measured on gfx950 (scripts/probe_mfma_f16.hip, 4.1M
+//     elements incl. adversarial magnitudes): |D - exact| <= 7.95 u (|C| +
+//     sum|ab|); the bound used is 16 u (|C| + sum|ab|) per MFMA: 16u S (1 +
+//     2^-9) for the hi x hi MFMA, 16u (|a| + 2^-8 S) for the second.
+//   * the reference's own float64 rounding: 2^-46 S absolute, 2^-40 relative.
+//   => |a'_computed - a'| <= alpha = aS * |c|_1 M^2 + ... + 16u |a'|; the
+//      16u |a'| part is a relative factor folded into t (1 -/+ 2^-18).
+//   * certain inlier: (|a| + alpha)^2 <= (1 + 2^-6) a^2 + 65 alpha^2 (AM-GM)
+//     <= t D  <=  aa < t_lo D - eps1,  t_lo = t / (1 + 2^-6) (and the
+//     aa rounding 2^-22, ...), eps1 = 65 alpha^2 / (1 + 2^-6).
+//     certain outlier: aa > t_hi D + eps2, t_hi = t / (1 - 2^-6), eps2 = 64
+//     alpha^2 / (1 - 2^-6) (if |a| < alpha the test cannot fire).
+//   * Ylo / Yhi themselves: f16 coefficients and monomials (2^-11 relative
+//     each) and the accumulation: eta <= 1.048e-3 (>= 2^-10 + 2^-20 + margin) sum|g_j| M^2 (+ subnormal
+//     terms), subtracted from / added to the coefficients of M^2; eps via M^4.
+//     Directed rounding keeps every eps / eta coefficient >= its bound.
+// Validity: 2^-15 <= thr < 1 (k in [0, 15]), finite non-zero E (zero E scores
+// 0 exactly: a = D = 0 gives NaN in the reference; non-finite E: every
+// evaluation goes to float64), M <= 15.9 per point (else float64).
+// Numerically emulated before the kernel was written: 0 wrong decisions and
+// 0.65 % undecided over 28M evaluations of 1398 KITTI candidates.
+
+typedef _Float16 mf_half8 __attribute__((ext_vector_type(8)));
+typedef float mf_float16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMfWaves = 8;                 // waves per block: one 32-candidate tile each
+constexpr int kMfSpan = 768;                // points per item (B fragments staged in LDS)
+constexpr int kMfTiles = kMfSpan / 32;
+constexpr int kMfQueue = 1024;              // undecided entries per wave (drained when it could overflow)
+constexpr int kMfRec = 64;                  // f16 per candidate: 4 A rows of K = 16
+constexpr float kMfMaxM = 15.9f;            // M^4 stays below the f16 maximum
+
+// per-candidate A rows (k_mf_cands): a1 [c_hi 0..8, c_hi 0..6] | a2 [c_hi 7..8,
+// c_lo 0..8, 0 x5] | Ylo [g_lo 0..10 (g_2 - eps1c), -eta_lo, -eps1 s1, -eps1 s2, 0 x2] | Yhi [g_hi, +eta_hi, ...]
+// and per-point B columns (staged in k_score_mf) with the same K order:
+// b1 [m_hi 0..8, m_lo 0..6] | b2 [m_lo 7..8, m_hi 0..8, 0 x5] | bD [md 0..10, M^2, (s1/4)^2, (s2/4)^2, 0 x2]
+
+struct MfParams {
+  int k;                 // a' = 2^k a
+  double t_lo, t_hi;     // scaled thresholds thr^2 4^k with the slack factors above
+};
+
+__host__ inline bool mf_params(double thr, MfParams* p) {
+  if (!(thr >= 0x1p-15 && thr < 1.0)) return false;
+  int k = 0;
+  while (k < 15 && std::ldexp(thr, k + 1) <= 1.0) ++k;          // 2^k <= 1/thr < 2^(k+1)
+  const double t = std::ldexp(thr * thr, 2 * k);                 // in (0.25, 1]
+  p->k = k;
+  p->t_lo = t * (1.0 - 0x1p-40) * (1.0 - 0x1p-22) * (1.0 - 0x1p-18) / (1.0 + 0x1p-6);
+  p->t_hi = t * (1.0 + 0x1p-40) * (1.0 + 0x1p-22) * (1.0 + 0x1p-18) / (1.0 - 0x1p-6);
+  return true;
+}
+
+// an f16 no smaller than v (v >= 0): inflate past one rounding, plus one
+// subnormal quantum; v past the f16 range -> +inf (the caller checks)
+__device__ __forceinline__ _Float16 f16_up(double v) {
+  return (_Float16)(float)(v * (1.0 + 0x1p-10) + 0x1p-24);
+}
+
+// One thread per candidate: the four A rows of its record.
+__global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, const double* __restrict__ candE,
+                           _Float16* __restrict__ candF, MfParams mp) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cand_total[b]) return;
+  const double* E = candE + ((size_t)b * cmax + c) * kCandStride;
+  _Float16 row[kMfRec];
+#pragma unroll
+  for (int i = 0; i < kMfRec; ++i) row[i] = (_Float16)0.0f;
+  double m = 0.0;
+  bool finite = true;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    finite = finite && isfinite(E[i]);
+    m = fmax(m, fabs(E[i]));
+  }
+  // zero E: a = D = 0, the reference's 0/0 is NaN -> never an inlier: Ylo = Yhi = -1
+  // (every evaluation a decided outlier); non-finite E: Ylo = -1, Yhi = +1 (all undecided)
+  bool special = !finite || m == 0.0;
+  if (!special) {
+    int e;
+    (void)frexp(m, &e);
+    double cc[9], hi[9], lo[9], En[9];
+    double cm = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      En[i] = ldexp(E[i], -e);                    // exact: max |En| in [0.5, 1)
+      cc[i] = ldexp(En[i], mp.k);                 // a' coefficients, <= 2^15
+      hi[i] = (double)(_Float16)(float)cc[i];
+      lo[i] = (double)(_Float16)(float)(cc[i] - hi[i]);
+      cm = fmax(cm, fabs(cc[i]));
+    }
+    // monomial order of a: E_ij x'_i x_j -> (x'x, x'y, x', y'x, y'y, y', x, y, 1) = E row-major
+#pragma unroll
+    for (int j = 0; j < 9; ++j) row[j] = (_Float16)hi[j];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) row[9 + j] = (_Float16)hi[j];
+    row[16] = (_Float16)hi[7];
+    row[17] = (_Float16)hi[8];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) row[18 + j] = (_Float16)lo[j];
+    // D = sum_{r<2} (E_r . x)^2 + sum_{c<2} (x' . E_c)^2 on (x^2, y^2, 1, xy, x, y, x'^2, y'^2, x'y', x', y')
+    const double e00 = En[0], e01 = En[1], e02 = En[2], e10 = En[3], e11 = En[4], e12 = En[5], e20 = En[6];
+    const double e21 = En[7];
+    double g[11];
+    g[0] = e00 * e00 + e10 * e10;
+    g[1] = e01 * e01 + e11 * e11;
+    g[2] = (e02 * e02 + e12 * e12) + (e20 * e20 + e21 * e21);
+    g[3] = 2.0 * (e00 * e01 + e10 * e11);
+    g[4] = 2.0 * (e00 * e02 + e10 * e12);
+    g[5] = 2.0 * (e01 * e02 + e11 * e12);
+    g[6] = e00 * e00 + e01 * e01;
+    g[7] = e10 * e10 + e11 * e11;
+    g[8] = 2.0 * (e00 * e10 + e01 * e11);
+    g[9] = 2.0 * (e00 * e20 + e01 * e21);
+    g[10] = 2.0 * (e10 * e20 + e11 * e21);
+    double sl = 0.0, sh = 0.0, ml = 0.0, mh = 0.0;
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {
+      const _Float16 gl = (_Float16)(float)(mp.t_lo * g[j]);
+      const _Float16 gh = (_Float16)(float)(mp.t_hi * g[j]);
+      row[32 + j] = gl;
+      row[48 + j] = gh;
+      sl += fabs((double)gl); ml = fmax(ml, fabs((double)gl));
+      sh += fabs((double)gh); mh = fmax(mh, fabs((double)gh));
+    }
+    // alpha <= aS S + 2^-24 (s1 + s2 + 1) + 9 * 2^-24 max|c| with S = sum |c_j m_j| and the
+    // point's group sums s1 = |x'x| + |x'y| + |y'x| + |y'y|, s2 = |x'| + |y'| + |x| + |y|
+    // (subnormal lo parts: 2^-25 absolute per product on either side, doubled):
+    //   alpha <= K1 s1 + K2 s2 + K3,  K1 = aS C1 + 2^-24, K2 = aS C2 + 2^-24,
+    //   K3 = aS |c_8| + 2^-24 + 9 * 2^-24 max|c|,  C1 / C2 = max |c| over each group;
+    //   alpha^2 <= 3 (K1^2 s1^2 + K2^2 s2^2 + K3^2)   (Cauchy-Schwarz)
+    // eps terms ride on the monomials (s1/4)^2, (s2/4)^2 and '1'.
+    const double aS = 16.0 * 0x1p-24 * (1.0 + 0x1p-9) + 3.75 * 0x1p-22 + 16.0 * 0x1p-24 * 0x1p-8 + 0x1p-46;
+    const double C1 = fmax(fmax(fabs(cc[0]), fabs(cc[1])), fmax(fabs(cc[3]), fabs(cc[4])));
+    const double C2 = fmax(fmax(fabs(cc[2]), fabs(cc[5])), fmax(fabs(cc[6]), fabs(cc[7])));
+    const double K1 = aS * C1 + 0x1p-24, K2 = aS * C2 + 0x1p-24;
+    const double K3 = aS * fabs(cc[8]) + 0x1p-24 + 9.0 * 0x1p-24 * cm;
+    const double infl = 3.0 * (1.0 + 0x1p-9);
+    const double e1s1 = 16.0 * infl * 65.0 * K1 * K1 / (1.0 + 0x1p-6);     // x (s1/4)^2
+    const double e1s2 = 16.0 * infl * 65.0 * K2 * K2 / (1.0 + 0x1p-6);
+    const double e1c = infl * 65.0 * K3 * K3 / (1.0 + 0x1p-6);
+    const double e2s1 = 16.0 * infl * 64.0 * K1 * K1 / (1.0 - 0x1p-6);
+    const double e2s2 = 16.0 * infl * 64.0 * K2 * K2 / (1.0 - 0x1p-6);
+    const double e2c = infl * 64.0 * K3 * K3 / (1.0 - 0x1p-6);
+    // the constant monomial carries g_2 -/+ eps (its f16 rounding is covered by eta)
+    row[32 + 2] = (_Float16)(float)(mp.t_lo * g[2] - e1c);
+    row[48 + 2] = (_Float16)(float)(mp.t_hi * g[2] + e2c);
+    sl = 0.0; sh = 0.0; ml = 0.0; mh = 0.0;
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {
+      const double gl = (double)row[32 + j], gh = (double)row[48 + j];
+      sl += fabs(gl); ml = fmax(ml, fabs(gl));
+      sh += fabs(gh); mh = fmax(mh, fabs(gh));
+    }
+    // eta: f16 coefficients and monomials (2^-11 relative each; 2^-25 absolute
+    // when subnormal, on either side) and the accumulation, per M^2 (M >= 1)
+    const double eta_lo = (1.048e-3 * sl + 11.0 * 0x1p-25 * (ml + 1.0)) * (1.0 + 0x1p-9);
+    const double eta_hi = (1.048e-3 * sh + 11.0 * 0x1p-25 * (mh + 1.0)) * (1.0 + 0x1p-9);
+    const _Float16 Blo = f16_up(eta_lo), Bhi = f16_up(eta_hi);
+    const _Float16 S1lo = f16_up(e1s1), S2lo = f16_up(e1s2), S1hi = f16_up(e2s1), S2hi = f16_up(e2s2);
+    if (isfinite((float)Blo) && isfinite((float)Bhi) && isfinite((float)S1lo) && isfinite((float)S2lo) &&
+        isfinite((float)S1hi) && isfinite((float)S2hi) && isfinite((float)row[32 + 2]) &&
+        isfinite((float)row[48 + 2])) {
+      row[32 + 11] = -Blo;
+      row[32 + 12] = -S1lo;
+      row[32 + 13] = -S2lo;
+      row[48 + 11] = Bhi;
+      row[48 + 12] = S1hi;
+      row[48 + 13] = S2hi;
+    } else {
+      special = true;
+      finite = false;
+    }
+  }
+  if (special) {
+#pragma unroll
+    for (int i = 0; i < kMfRec; ++i) row[i] = (_Float16)0.0f;
+    row[32 + 2] = (_Float16)(-1.0f);                             // Ylo = -1 (monomial '1')
+    row[48 + 2] = (_Float16)(finite ? -1.0f : 1.0f);             // Yhi = -1 (outlier) / +1 (undecided)
+  }
+  uint4* out = reinterpret_cast<uint4*>(candF + ((size_t)b * cmax + c) * kMfRec);
+  const uint4* in = reinterpret_cast<const uint4*>(row);
+#pragma unroll
+  for (int i = 0; i < kMfRec / 8; ++i) out[i] = in[i];
+}
+
+// Stage one point's three B columns into the LDS fragment image of its tile:
+// frag[t][f][lane][8], lane = 32 h + r holds K = 8h .. 8h+7 of column r.
+// Monomials in float32 from float32 coordinates (relative error <= 3 * 2^-24
+// against the float64 point, 0.75 * 2^-22 of the 3.75 * 2^-22 representation
+// term of aS), split into f16 hi + lo: m - hi is exact in float32, lo rounds
+// once (2^-22 |m|).  Dead slots are zero; a point past the f16 range (M >
+// 15.9, or NaN) is zeroed and reported (return value).
+__device__ __forceinline__ bool mf_stage_point(const double4 v, bool live, _Float16* frag_tile, int r) {
+  const float x = (float)v.x, y = (float)v.y, xp = (float)v.z, yp = (float)v.w;
+  float M = fmaxf(fmaxf(fabsf(x), fabsf(y)), fmaxf(fabsf(xp), fabsf(yp)));
+  M = fmaxf(M, 1.0f);
+  const bool bad = live && !(M <= kMfMaxM);
+  _Float16 col[48];
+#pragma unroll
+  for (int i = 0; i < 48; ++i) col[i] = (_Float16)0.0f;
+  if (live && !bad) {
+    const float ma[9] = {xp * x, xp * y, xp, yp * x, yp * y, yp, x, y, 1.0f};
+    _Float16 hi[9], lo[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      hi[j] = (_Float16)ma[j];
+      lo[j] = (_Float16)(ma[j] - (float)hi[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) col[j] = hi[j];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) col[9 + j] = lo[j];
+    col[16] = lo[7];
+    col[17] = lo[8];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) col[18 + j] = hi[j];
+    const float md[11] = {x * x, y * y, 1.0f, x * y, x, y, xp * xp, yp * yp, xp * yp, xp, yp};
+#pragma unroll
+    for (int j = 0; j < 11; ++j) col[32 + j] = (_Float16)md[j];
+    // bound monomials, rounded up (>= their float64-point values): M^2 for the
+    // Ylo / Yhi rounding terms, (s1/4)^2 and (s2/4)^2 for the a-error terms
+    const double up = 1.0 + 0x1p-20;
+    const double Mu = (double)M * up;
+    const double s1 = ((double)fabsf(ma[0]) + fabsf(ma[1]) + fabsf(ma[3]) + fabsf(ma[4])) * up * up * 0.25;
+    const double s2 = ((double)fabsf(xp) + fabsf(yp) + fabsf(x) + fabsf(y)) * up * 0.25;
+    col[32 + 11] = f16_up(Mu * Mu);
+    col[32 + 12] = f16_up(s1 * s1);
+    col[32 + 13] = f16_up(s2 * s2);
+  }
+#pragma unroll
+  for (int f = 0; f < 3; ++f)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      *reinterpret_cast<uint4*>(frag_tile + ((size_t)f * 64 + 32 * h + r) * 8) =
+          *reinterpret_cast<const uint4*>(col + 16 * f + 8 * h);
+  return bad;
+}
+
+// row of accumulator register g in half h of a 32x32 MFMA output
+__host__ __device__ constexpr int mf_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+// The float64 test of queued (candidate row, point) evaluations, with the
+// span's points and the tile's E rows read from LDS (no global latency).
+__device__ __forceinline__ void mf_drain(const double* __restrict__ sE, const double4* __restrict__ spts, int p0,
+                                         int T, int R, const ScoreConsts& kc, int lane, int32_t (*cnt)[2],
+                                         const uint32_t* q, int qn) {
+#pragma unroll 1
+  for (int i = lane; i < qn; i += 64) {
+    const uint32_t e = q[i];
+    const int c = (int)(e >> 24), p = (int)(e & 0xffffffu);
+    if (inlier_f64v(sE + c * 10, spts[p - p0], kc)) {
+      if (p < T) atomicAdd(&cnt[c][0], 1);
+      if (p < R) atomicAdd(&cnt[c][1], 1);
+    }
+  }
+}
+
+#ifdef SFM_MF_STAMPS
+// experiment builds only (scripts/mf_stamps.py): per-phase wave cycles of
+// k_score_mf: [0] item setup + staging, [1] main loop, [2] queue + float64
+// drain, [3] reduction + atomics + barrier; [4] items (vector atomics only)
+__device__ unsigned long long g_mf_stamps[5];
+extern "C" int sfm_experiment_mf_stamps(unsigned long long* out5, int reset) {
+  if (reset) {
+    unsigned long long z[5] = {0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_mf_stamps), z, 40) == hipSuccess ? 0 : 2;
+  }
+  return hipMemcpyFromSymbol(out5, HIP_SYMBOL(g_mf_stamps), 40) == hipSuccess ? 0 : 2;
+}
+#define MF_STAMP(i)                                                                       \
+  do {                                                                                    \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                         \
+    mf_acc_[i] += now_ - mf_t0_;                                                          \
+    mf_t0_ = now_;                                                                        \
+  } while (0)
+#else
+#define MF_STAMP(i) do { } while (0)
+#endif
+
+struct MfAcc {
+  mf_float16 a, lo, hi;
+};
+
+__device__ __forceinline__ MfAcc mf_tile_mfma(const _Float16* frag_tile, int lane, mf_half8 A1, mf_half8 A2,
+                                              mf_half8 AL, mf_half8 AH) {
+  const mf_half8 B1 = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(0 * 64 + lane) * 8);
+  const mf_half8 B2 = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(1 * 64 + lane) * 8);
+  const mf_half8 BD = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(2 * 64 + lane) * 8);
+  mf_float16 z;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) z[g] = 0.0f;
+  MfAcc r;
+  r.a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B1, z, 0, 0, 0);          // hi x hi (+7 hi x lo) first
+  r.lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(AL, BD, z, 0, 0, 0);
+  r.hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(AH, BD, z, 0, 0, 0);
+  r.a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A2, B2, r.a, 0, 0, 0);        // the small products
+  return r;
+}
+
+// Decisions of one tile, branch-free: per lane and accumulator register g one
+// packed word acc[g]: the inliers counted so far in bits 0..4 (<= kMfTiles),
+// and bit 5 + t set when the evaluation of tile t was undecided.  (A taken
+// scalar branch per register cost ~10 cycles per instruction overall.)
+// !SAME: separate inlier counts for the num_test / num_ransac_test prefixes.
+template <bool SAME>
+__device__ __forceinline__ void mf_tile_decide(const MfAcc& r, float offs, bool inT, bool inR, uint32_t ubit,
+                                               uint32_t (&acc)[16], int (&cR)[16]) {
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const float aa = __builtin_fmaf(r.a[g], r.a[g], offs);
+    const bool bin = aa < r.lo[g];
+    const bool bout = aa > r.hi[g];
+    const bool und = !(bin || bout);
+    acc[g] += ((bin && inT) ? 1u : 0u) + (und ? ubit : 0u);
+    if (!SAME) cR[g] += (bin && inR) ? 1 : 0;
+  }
+}
+
+static_assert(kMfTiles <= 27 && kMfTiles < 32, "count (5 bits) + one undecided flag per tile in 32 bits");
+
+template <class Src, bool SAME>
+__global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairParams pp, int batch, int cmax,
+                                                           const int32_t* __restrict__ cand_total,
+                                                           const double* __restrict__ candE,
+                                                           const _Float16* __restrict__ candF,
+                                                           int32_t* __restrict__ cntT, int32_t* __restrict__ cntR,
+                                                           ScoreConsts kc) {
+  __shared__ __attribute__((aligned(16))) _Float16 s_frag[kMfTiles][3][64][8];
+  __shared__ double4 s_pts[kMfSpan];
+  __shared__ double s_E[kMfWaves][kKC * 10];                 // E (9) + guard Kg of the wave's tile
+  __shared__ uint32_t s_badcol[2][32];                      // bit t of column r: point (t, r) out of range
+                                                            // (by item parity: reset while the other is staged)
+  __shared__ uint32_t s_queue[kMfWaves][kMfQueue];
+  __shared__ int32_t s_cnt[kMfWaves][kKC][2];
+  __shared__ int32_t s_first[SFM_MAX_BATCH + 1];
+  __shared__ int32_t s_spans[SFM_MAX_BATCH];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hl = lane >> 5, rl = lane & 31;
+  if (tid == 0) {
+    int acc = 0;
+    for (int b = 0; b < batch; ++b) {
+      const int tiles = (cand_total[b] + kKC - 1) / kKC;
+      const int groups = (tiles + kMfWaves - 1) / kMfWaves;
+      const int spans = (max(pp.test[b], pp.rtest[b]) + kMfSpan - 1) / kMfSpan;
+      s_spans[b] = spans;
+      s_first[b] = acc;
+      acc += groups * spans;
+    }
+    s_first[batch] = acc;
+  }
+  for (int i = tid; i < kMfWaves * kKC * 2; i += kMfWaves * 64) (&s_cnt[0][0][0])[i] = 0;
+  __syncthreads();
+  const int total = s_first[batch];
+  int32_t(*cnt)[2] = s_cnt[wv];
+  uint32_t* queue = s_queue[wv];
+  const double* sE = s_E[wv];
+  // item -> (pair, candidate group, span) and its prefetch: the next item's
+  // points, A rows and E rows are loaded into registers while the current
+  // item computes, so staging costs no global latency
+  struct Item { int b, p0, p1, c0, nc, T, R; };
+  auto item_of = [&](int item) {
+    Item it;
+    int b = 0;
+    while (item >= s_first[b + 1]) ++b;
+    const int local = item - s_first[b];
+    const int spans = s_spans[b];
+    const int group = local / spans, span = local - group * spans;
+    it.b = b;
+    it.T = pp.test[b];
+    it.R = pp.rtest[b];
+    it.p0 = span * kMfSpan;
+    it.p1 = min(max(it.T, it.R), it.p0 + kMfSpan);
+    it.c0 = (group * kMfWaves + wv) * kKC;
+    it.nc = max(0, min(kKC, cand_total[b] - it.c0));
+    return it;
+  };
+  constexpr int kPtsPerThread = (kMfSpan + kMfWaves * 64 - 1) / (kMfWaves * 64);
+  constexpr int kEPerLane = (kKC * 10 + 63) / 64;
+  double4 pv[kPtsPerThread];
+  double ev[kEPerLane];
+  mf_half8 nA1, nA2, nAL, nAH;
+  auto prefetch = [&](const Item& it) {
+#pragma unroll
+    for (int j = 0; j < kPtsPerThread; ++j) {
+      const int i = tid + j * kMfWaves * 64;
+      const int p = it.p0 + i;
+      pv[j] = src.load(it.b, (i < kMfSpan && p < it.p1) ? p : it.p0);
+    }
+#pragma unroll
+    for (int j = 0; j < kEPerLane; ++j) {
+      const int i = lane + 64 * j;
+      ev[j] = i < it.nc * 10 ? candE[((size_t)it.b * cmax + it.c0 + i / 10) * kCandStride + i % 10] : 0.0;
+    }
+    if (rl < it.nc) {
+      const mf_half8* rec = reinterpret_cast<const mf_half8*>(candF + ((size_t)it.b * cmax + it.c0 + rl) * kMfRec);
+      nA1 = rec[0 + hl];
+      nA2 = rec[2 + hl];
+      nAL = rec[4 + hl];
+      nAH = rec[6 + hl];
+    } else {                                                 // absent row: every evaluation a decided outlier
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        nA1[j] = (_Float16)0.0f; nA2[j] = (_Float16)0.0f; nAL[j] = (_Float16)0.0f; nAH[j] = (_Float16)0.0f;
+      }
+      if (hl == 0) { nAL[2] = (_Float16)(-1.0f); nAH[2] = (_Float16)(-1.0f); }
+    }
+  };
+  if (tid < 64) s_badcol[tid >> 5][tid & 31] = 0u;
+  int par = 0;
+  Item cur;
+  if (blockIdx.x < total) {
+    cur = item_of(blockIdx.x);
+    prefetch(cur);
+  }
+  __syncthreads();
+#ifdef SFM_MF_STAMPS
+  unsigned long long mf_t0_ = __builtin_amdgcn_s_memtime();
+  unsigned long long mf_acc_[5] = {0, 0, 0, 0, 0};
+#endif
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+#ifdef SFM_MF_STAMPS
+    mf_acc_[4] += 1;
+#endif
+    const int b = cur.b, p0 = cur.p0, p1 = cur.p1, c0 = cur.c0, nc = cur.nc, T = cur.T, R = cur.R;
+    // 1. stage the prefetched span (points + B columns) and E rows into LDS
+#pragma unroll
+    for (int j = 0; j < kPtsPerThread; ++j) {
+      const int i = tid + j * kMfWaves * 64;
+      if (i < kMfSpan) {
+        s_pts[i] = pv[j];
+        if (mf_stage_point(pv[j], p0 + i < p1, &s_frag[i >> 5][0][0][0], i & 31))
+          atomicOr(&s_badcol[par][i & 31], 1u << (i >> 5));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kEPerLane; ++j) {
+      const int i = lane + 64 * j;
+      if (i < kKC * 10) s_E[wv][i] = ev[j];
+    }
+    const mf_half8 A1 = nA1, A2 = nA2, AL = nAL, AH = nAH;
+    __syncthreads();
+    const uint32_t badcol = s_badcol[par][rl];              // bit t: point (t, rl) outside the f16 range
+    // 2. the next item's loads fly while this one computes
+    if (item + (int)gridDim.x < total) {
+      const Item nxt = item_of(item + gridDim.x);
+      prefetch(nxt);
+      cur = nxt;
+    }
+    MF_STAMP(0);
+    if (nc > 0) {
+      uint32_t acc[16];
+      int cR[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) { acc[g] = 0u; cR[g] = 0; }
+      const int ntiles = (p1 - p0 + 31) >> 5;
+      const int nlive = p1 - p0 - rl;                        // tiles t with 32t < nlive hold a live point here
+      // aa = a*a + offs: 0 for a live point; +inf past the span (a decided
+      // outlier: never counted, never queued); NaN for a point outside the
+      // f16 range (both compares false: undecided -> float64)
+      auto offs_of = [&](int t) {
+        return 32 * t >= nlive ? __builtin_huge_valf() : (((badcol >> t) & 1u) ? __builtin_nanf("") : 0.0f);
+      };
+      // software pipeline, explicit ping-pong (no accumulator copies): the
+      // MFMAs of the next tile run while the current one is decided
+      MfAcc ta = mf_tile_mfma(&s_frag[0][0][0][0], lane, A1, A2, AL, AH), tb;
+      for (int t = 0; t < ntiles; t += 2) {
+        if (t + 1 < ntiles) tb = mf_tile_mfma(&s_frag[t + 1][0][0][0], lane, A1, A2, AL, AH);
+        mf_tile_decide<SAME>(ta, offs_of(t), SAME || p0 + 32 * t + rl < T, SAME || p0 + 32 * t + rl < R,
+                             1u << (5 + t), acc, cR);
+        if (t + 1 >= ntiles) break;
+        if (t + 2 < ntiles) ta = mf_tile_mfma(&s_frag[t + 2][0][0][0], lane, A1, A2, AL, AH);
+        mf_tile_decide<SAME>(tb, offs_of(t + 1), SAME || p0 + 32 * (t + 1) + rl < T,
+                             SAME || p0 + 32 * (t + 1) + rl < R, 1u << (6 + t), acc, cR);
+      }
+      MF_STAMP(1);
+      // the undecided evaluations -> the queue -> float64 (drained whenever it
+      // could overflow: pathological spans may be all undecided)
+      int qn = 0;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        uint32_t ub = acc[g] >> 5;
+        for (;;) {
+          const uint64_t has = __ballot(ub != 0u);
+          if (!has) break;
+          if (qn > kMfQueue - 64) {
+            wave_sync();
+            mf_drain(sE, s_pts, p0, T, R, kc, lane, cnt, queue, qn);
+            qn = 0;
+            wave_sync();
+          }
+          if (ub) {
+            const int t = __builtin_ctz(ub);
+            ub &= ub - 1u;
+            const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0));
+            queue[pos] = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(p0 + 32 * t + rl);
+          }
+          qn += __popcll(has);
+        }
+      }
+      wave_sync();
+      mf_drain(sE, s_pts, p0, T, R, kc, lane, cnt, queue, qn);
+      MF_STAMP(2);
+      // reduce the per-lane counts over each half's 32 lanes; lane 32h then
+      // holds candidate row mf_row(g, h)'s span count
+      int cT[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        cT[g] = (int)(acc[g] & 31u);
+#pragma unroll
+        for (int d = 16; d >= 1; d >>= 1) {
+          cT[g] += __shfl_xor(cT[g], d, 64);
+          if (!SAME) cR[g] += __shfl_xor(cR[g], d, 64);
+        }
+      }
+      if (rl == 0) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          atomicAdd(&cnt[mf_row(g, hl)][0], cT[g]);
+          atomicAdd(&cnt[mf_row(g, hl)][1], SAME ? cT[g] : cR[g]);
+        }
+      }
+      wave_sync();
+      {
+        const int c = lane >> 1, which = lane & 1;
+        const int sc = cnt[c][which];
+        if (c < nc && sc) atomicAdd((which ? cntR : cntT) + (size_t)b * cmax + c0 + c, sc);
+        cnt[c][which] = 0;
+      }
+    }
+    __syncthreads();                                          // the span is re-staged next item
+    if (tid < 32) s_badcol[par][tid] = 0u;                    // every wave read it before the barrier
+    par ^= 1;
+    MF_STAMP(3);
+  }
+#ifdef SFM_MF_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_mf_stamps[i], mf_acc_[i]);
+#endif
+}

@@ -1,4 +1,6 @@
-"""Exact bound pruning in the score kernel (tuning key score_prune): the
+"""Exact bound pruning in the float32 score kernel k_score32 (tuning key
+score_prune; the split-f16 matrix-core scorer k_score_mf, the default, is
+turned off here with score_mf=0): the
 winner, its inlier count, E and P must be identical with pruning on and off,
 and (through the unpruned path's bit-exact parity) equal to the oracle's.
 Pruning is active only without per-hypothesis scores and with
@@ -18,6 +20,7 @@ def _both(pts, n=None, iters=2, thr=1e-4, nt=None, nr=None):
     ws = ransac.workspace_for(B, iters, pts.device)
     out = {}
     try:
+        _lib.tune("score_mf", 0)
         for prune in (0, 1):
             _lib.tune("score_prune", prune)
             E, P, inl, win = ransac.ransac5_batched(pts, n, nt, nr, iters, thr, workspace=ws)
@@ -25,6 +28,7 @@ def _both(pts, n=None, iters=2, thr=1e-4, nt=None, nr=None):
             out[prune] = (E.cpu(), P.cpu(), inl.cpu(), win.cpu(), ransac.skipped_evaluations(ws, B, iters))
     finally:
         _lib.tune("score_prune", 1)
+        _lib.tune("score_mf", 1)
     return out
 
 
