@@ -91,7 +91,8 @@ int sfm_tune_set(const char* key, int value) {
   else if (k == "sweep_lane_pixels" && value >= 0 && value <= 2) t.sweep_lane_pixels = value;
   else if (k == "sweep_items_per_block" && (value == 1 || value == 2 || value == 4 || value == 8))
     t.sweep_items_per_block = value;
-  else if (k == "sweep_flat" && (value == 0 || value == 1)) t.sweep_flat = value;
+  else if (k == "sweep_flat" && value >= 0 && value <= 2) t.sweep_flat = value;
+  else if (k == "sweep_nj" && (value == 1 || value == 2 || value == 4)) t.sweep_nj = value;
   else if (k == "sweep_group" && (value == 4 || value == 8)) t.sweep_group = value;
   else if (k == "score_blocks_per_cu" && value >= 1 && value <= 64) t.score_blocks_per_cu = value;
   else if (k == "score_fp32" && (value == 0 || value == 1)) t.score_fp32 = value;

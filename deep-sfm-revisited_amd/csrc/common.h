@@ -15,7 +15,8 @@ struct Tuning {
   int roots_lanes = 32;          // active lanes per k_roots wave (1..64)
   int sweep_items_per_block = 4; // consecutive (row, plane, window) items per sweep block
   int sweep_lane_pixels = 0;     // 1: warped lanes own 4 consecutive pixels (16-byte stores)
-  int sweep_flat = 1;            // 1: 256-byte-aligned slab windows (k_sweep_flat); 0: per-row windows
+  int sweep_flat = 2;            // 1: 256-byte-aligned slab windows (k_sweep_flat); 2: narrow windows (k_sweep_tile); 0: per-row
+  int sweep_nj = 1;              // k_sweep_tile (sweep_flat = 2): pixels per lane, window 256 * nj (bf16: even)
   int sweep_group = 8;           // warped channels per k_sweep_flat item (4 or 8; 8 measured stable in the bench loop)
   int score_blocks_per_cu = 32;  // persistent score grid
   int score_fp32 = 1;            // packed float32 pre-decision in the score kernel

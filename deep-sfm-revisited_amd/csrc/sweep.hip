@@ -524,6 +524,197 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_flat(const float* __restri
     sweep_flat_item<OutT, NQ, false>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
 }
 
+// ---------------------------------------------------------------------------
+// Cost volume, narrow-window form (tuning key sweep_flat = 2).
+//
+// The same aligned slab windows as k_sweep_flat, but a window is 256 * NJ
+// elements and every lane owns NJ lane-consecutive pixels (wave pixel
+// 64 j + lane), for both output types:
+//   * HBM write rate on MI355X falls with the bytes that the resident
+//     workgroups have in flight at once (profiles/r01_probe_store_bw2.txt:
+//     items of 1 / 4 / 8 / 16 rows x 4 KB: 6.7 / 6.5 / 6.3 / 5.7 TB/s; one
+//     contiguous span of 4 KB vs 64 KB per block: 7.0 vs 6.0 TB/s).  An item
+//     writes 2G rows; NJ = 1 keeps it at 2G x 1 KB.
+//   * bf16: neighbouring lanes' pixels are packed into 4-byte pairs with one
+//     DPP quad swap (lane 2k stores pixels 64 j + 2k, +1 of register j = 2s,
+//     lane 2k + 1 those of register 2s + 1), so the gathers stay
+//     lane-consecutive and each wave store is still one 256-byte segment.
+// ---------------------------------------------------------------------------
+template <typename OutT> struct TileLanes;
+template <> struct TileLanes<float> { static constexpr int AM = 63; };
+template <> struct TileLanes<unsigned short> { static constexpr int AM = 127; };
+
+__device__ __forceinline__ unsigned bf16_pair_swap(unsigned a, unsigned b, bool odd) {
+  // a, b: this lane's bf16 of pixel registers 2s and 2s+1; returns the pair
+  // (lo, hi) this lane stores: even lane (a_self, a_next), odd (b_prev, b_self)
+  const unsigned send = odd ? a : b;
+  const unsigned r = (unsigned)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  return odd ? (r | (b << 16)) : (a | (r << 16));
+}
+
+template <typename OutT, int NQ, int NJ, bool INTERIOR>
+__device__ __forceinline__ void sweep_tile_item(const float* __restrict__ ref, const f32x4* __restrict__ tq,
+                                                const float* __restrict__ pose,
+                                                const float* __restrict__ K4, const float* __restrict__ K4inv,
+                                                const FlatGeom& g, OutT* __restrict__ out, int b, int k,
+                                                int start, size_t wbase) {
+  constexpr bool BF = sizeof(OutT) == 2;
+  static_assert(!BF || NJ % 2 == 0, "bf16 windows pack register pairs");
+  constexpr int G = 4 * NQ, WW = 64 * NJ;
+  const int c0 = k * G;
+  const int l0 = (int)magic_div((unsigned)max(start, 0), g.mhw);
+  const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+  const int woff = start + WW * wave;                 // slab index of the wave's first pixel
+  int ps[NJ], ls[NJ];
+  bool okf[NJ];
+  const int pbase = start - l0 * g.hw;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int f = woff + 64 * j + lane;
+    int p = pbase + WW * wave + 64 * j + lane, l = l0;
+    okf[j] = true;
+    if (!INTERIOR) {
+      okf[j] = f >= 0 && f < g.slab;
+      if (!okf[j]) p = 0;
+    }
+    while (p >= g.hw) { p -= g.hw; ++l; }
+    ps[j] = p;
+    ls[j] = l;
+  }
+  const int nc = min(G, g.C - c0);
+  float cp[G][NJ];
+  if (g.ref_rows) {
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      if (c >= nc) break;
+      const float* R = ref + ((size_t)b * g.C + c0 + c) * g.hw;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) cp[c][j] = *at_u32(R, (unsigned)ps[j] * 4u);
+    }
+  }
+  Proj pr;
+  load_proj(pose, K4, K4inv, b, pr);
+  const SampleK sk = sample_consts(g.h, g.w);
+  const float dA = plane_depth(g.dmax, g.dstep, l0), dB = plane_depth(g.dmax, g.dstep, l0 + 1);
+  const f32x4* Tb = tq + ((size_t)b * g.C4 + k * NQ) * g.hw;
+  f32x4 acc[NQ][NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int p = ps[j], l = ls[j];
+    float d = l == l0 ? dA : dB;
+    if (l > l0 + 1) d = plane_depth(g.dmax, g.dstep, l);
+    int y = (int)((float)p * g.inv_w);
+    int x = p - y * g.w;
+    if (x < 0) { --y; x += g.w; }
+    if (x >= g.w) { ++y; x -= g.w; }
+    const float xf = (float)x, yf = (float)y;
+    float ray[3];
+    ray[0] = (pr.ki[0] * xf + pr.ki[1] * yf) + pr.ki[2];
+    ray[1] = (pr.ki[3] * xf + pr.ki[4] * yf) + pr.ki[5];
+    ray[2] = (pr.ki[6] * xf + pr.ki[7] * yf) + pr.ki[8];
+    float ix, iy;
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) acc[n][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (sample_pos_nr(pr, ray, d, sk, ix, iy)) {
+      TapsIn tp;
+      make_taps_inside(ix, iy, g.h, g.w, tp);
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        if (4 * n >= nc) break;
+        const f32x4* T = Tb + (size_t)n * g.hw;
+        const f32x4 t0 = *at_u32(T, tp.off[0] * 16u), t1 = *at_u32(T, tp.off[1] * 16u);
+        const f32x4 t2 = *at_u32(T, tp.off[2] * 16u), t3 = *at_u32(T, tp.off[3] * 16u);
+        f32x4 a;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = tp.wt[0] * t0[e];
+          v = __builtin_fmaf(tp.wt[1], t1[e], v);
+          v = __builtin_fmaf(tp.wt[2], t2[e], v);
+          a[e] = __builtin_fmaf(tp.wt[3], t3[e], v);
+        }
+        acc[n][j] = a;
+      }
+    }
+  }
+  const bool odd = (lane & 1) != 0;
+  auto store_row = [&](OutT* row, const float* v) {
+    if (!BF) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int f = woff + 64 * j + lane;
+        if (INTERIOR || okf[j]) store1(at_u32(row, (unsigned)f * 4u), v[j]);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < NJ / 2; ++s) {
+        const unsigned a = to_bf16(v[2 * s]), bb = to_bf16(v[2 * s + 1]);
+        const unsigned u = bf16_pair_swap(a, bb, odd);
+        // even lane 2k: pixels 128 s + 2k, +1; odd lane 2k+1: 128 s + 64 + 2k, +1
+        const int f = woff + 128 * s + lane + (odd ? 63 : 0);
+        if (INTERIOR && g.pair_ok) {
+          *reinterpret_cast<unsigned int*>(at_u32(row, (unsigned)f * 2u)) = u;
+        } else {
+          const bool okl = f >= 0 && f < g.slab, okh = f + 1 >= 0 && f + 1 < g.slab;
+          if (g.pair_ok && okl && okh) {
+            *reinterpret_cast<unsigned int*>(row + f) = u;
+          } else {
+            if (okl) row[f] = (unsigned short)(u & 0xffffu);
+            if (okh) row[f + 1] = (unsigned short)(u >> 16);
+          }
+        }
+      }
+    }
+  };
+  if (g.ref_rows) {
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      if (c >= nc) break;
+      store_row(out + ((size_t)b * g.rows + c0 + c) * (size_t)g.slab, cp[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < G; ++c) {
+    if (c >= nc) break;
+    float v[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) v[j] = acc[c >> 2][j][c & 3];
+    store_row(out + wbase + (size_t)c * g.slab, v);
+  }
+}
+
+template <typename OutT, int NQ, int NJ>
+__global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restrict__ ref,
+                                                           const f32x4* __restrict__ tq,
+                                                           const float* __restrict__ pose,
+                                                           const float* __restrict__ K4,
+                                                           const float* __restrict__ K4inv, FlatGeom g,
+                                                           OutT* __restrict__ out) {
+  constexpr int WIN = 256 * NJ;
+  const unsigned item = blockIdx.x;            // grid = B * groups * nwin
+  const unsigned r = magic_div(item, g.mwin);
+  const int win = (int)(item - r * (unsigned)g.nwin);
+  const int b = (int)magic_div(r, g.mgrp);
+  const int k = (int)(r - (unsigned)b * (unsigned)g.groups);
+  const size_t wbase = ((size_t)b * g.rows + g.ref_rows + k * 4 * NQ) * (size_t)g.slab;
+  const int start = win * WIN - (int)((wbase + (size_t)g.out_mis) & (size_t)g.amask);
+  if (start >= g.slab) return;
+  if (start >= 0 && start + WIN <= g.slab)
+    sweep_tile_item<OutT, NQ, NJ, true>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
+  else
+    sweep_tile_item<OutT, NQ, NJ, false>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
+}
+
+template <typename OutT, int NQ>
+static void launch_k_sweep_tile_nj(int nj, unsigned blocks, hipStream_t s, const float* ref, const f32x4* tq,
+                                   const float* pose, const float* K4, const float* K4inv, const FlatGeom& g,
+                                   void* out) {
+  const dim3 grid(blocks), block(kSwThreads);
+  constexpr bool BF = sizeof(OutT) == 2;
+  if (nj >= 4) hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, 4>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
+  else if (nj == 2 || BF) hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, 2>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
+  else hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, (BF ? 2 : 1)>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
+}
+
 template <typename OutT>
 static void launch_k_sweep_flat(int nq, unsigned blocks, hipStream_t s, const float* ref, const f32x4* tq,
                                 const float* pose, const float* K4, const float* K4inv, const FlatGeom& g,
@@ -645,8 +836,13 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   const int nq = tuning().sweep_group == 8 ? 2 : 1;
   const int64_t slab = (int64_t)L * hw;
   const int fgroups = (C + 4 * nq - 1) / (4 * nq);
-  const int64_t nwin = (slab + 127 + kFlatWin - 1) / kFlatWin;
-  if (tuning().sweep_flat && hw < (1 << 24) && slab < ((int64_t)1 << 30) && (int64_t)B * fgroups * nwin < ((int64_t)1 << 31)) {
+  const int mode = tuning().sweep_flat;
+  // k_sweep_tile: 256 * nj elements per window (bf16 packs register pairs: nj even)
+  int nj = tuning().sweep_nj;
+  if (out_dtype == 1 && nj < 2) nj = 2;
+  const int64_t win_el = mode == 2 ? 256 * (int64_t)nj : kFlatWin;
+  const int64_t nwin = (slab + 127 + win_el - 1) / win_el;
+  if (mode && hw < (1 << 24) && slab < ((int64_t)1 << 30) && (int64_t)B * fgroups * nwin < ((int64_t)1 << 31)) {
     FlatGeom fg;
     fg.B = B; fg.C = C; fg.C4 = g.C4; fg.h = h; fg.w = w; fg.L = L; fg.hw = hw;
     fg.ref_rows = g.ref_rows; fg.rows = g.rows; fg.G = 4 * nq; fg.groups = fgroups;
@@ -662,7 +858,15 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     fg.dmax = g.dmax; fg.dstep = g.dstep;
     const unsigned blocks = (unsigned)((int64_t)B * fgroups * nwin);
     ProfScope ps(pname, s);
-    if (out_dtype == 0) launch_k_sweep_flat<float>(nq, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+    if (mode == 2) {
+      if (out_dtype == 0) {
+        if (nq == 2) launch_k_sweep_tile_nj<float, 2>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+        else launch_k_sweep_tile_nj<float, 1>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+      } else {
+        if (nq == 2) launch_k_sweep_tile_nj<unsigned short, 2>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+        else launch_k_sweep_tile_nj<unsigned short, 1>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+      }
+    } else if (out_dtype == 0) launch_k_sweep_flat<float>(nq, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
     else launch_k_sweep_flat<unsigned short>(nq, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
     SFM_LAUNCHED();
     return SFM_OK;

@@ -1,5 +1,7 @@
-"""The aligned-slab sweep kernel (k_sweep_flat, the default) against the
-per-row kernel (tuning key sweep_flat=0) and the oracle: both group sizes,
+"""The aligned-slab sweep kernels (k_sweep_tile, the default, sweep_flat=2;
+k_sweep_flat, sweep_flat=1) against the per-row kernel (sweep_flat=0) and the
+oracle: both group sizes, every window width of k_sweep_tile (bit-identical to
+k_sweep_flat of the same group),
 edge windows, feature maps under one 1024-pixel window, odd slabs and output
 pointers off the 256-byte grid.  Sample positions are bit-identical
 (warp.h sample_pos_nr); the 4-tap sum differs by FMA rounding only."""
@@ -22,7 +24,7 @@ RTOL, FLOOR = 1e-4, 1.0    # the tolerance of test_gpu_sweep.py: 1e-4 * max(|b|,
     (1, 8, 4, 9, 13, torch.bfloat16, 2),       # even slab, output 4 B off: pair stores
     (1, 8, 8, 12, 25, torch.bfloat16, 4),      # even slab, output 8 B off
 ])
-def test_aligned_slab_kernel_matches_per_row(cuda, B, C, L, h, w, dtype, offset):
+def test_aligned_slab_kernels_match_per_row(cuda, B, C, L, h, w, dtype, offset):
     from sfm_amd import _lib, synth
     from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
     ref, tgt = synth.features(B, C, h, w, seed=C * L + w)
@@ -34,25 +36,32 @@ def test_aligned_slab_kernel_matches_per_row(cuda, B, C, L, h, w, dtype, offset)
     n = B * 2 * C * L * h * w
     outs = {}
     try:
-        for flat, group in ((0, 4), (1, 4), (1, 8)):
+        for flat, group, nj in ((0, 4, 1), (1, 4, 1), (1, 8, 1), (2, 4, 1), (2, 4, 2), (2, 4, 4),
+                                (2, 8, 1), (2, 8, 2), (2, 8, 4)):
             _lib.tune("sweep_flat", flat)
             _lib.tune("sweep_group", group)
+            _lib.tune("sweep_nj", nj)
             buf = torch.full((n + offset,), float("nan"), dtype=dtype, device=cuda)
             out = buf[offset:].view(B, 2 * C, L, h, w)
             plane_sweep_cost(*args, dtype=dtype, out=out)
-            outs[(flat, group)] = out.float().cpu()
+            outs[(flat, group, nj)] = out.float().cpu()
     finally:
-        _lib.tune("sweep_flat", 1)
+        _lib.tune("sweep_flat", 2)
         _lib.tune("sweep_group", 8)
-    base = outs[(0, 4)]
+        _lib.tune("sweep_nj", 1)
+    base = outs[(0, 4, 1)]
     assert not torch.isnan(base).any()
     tol = 2e-6 if dtype == torch.float32 else 1e-2
-    for key in ((1, 4), (1, 8)):
-        got = outs[key]
+    for key, got in outs.items():
+        if key[0] == 0:
+            continue
         assert not torch.isnan(got).any(), key            # every element written
         assert torch.equal(got[:, :C], base[:, :C]), key  # reference half: exact copy
         assert float((got - base).abs().max()) <= tol, (key, float((got - base).abs().max()))
+        if key[0] == 2:                                   # same arithmetic as k_sweep_flat
+            assert torch.equal(got, outs[(1, key[1], 1)]), key
     if dtype == torch.float32:
         want = S.plane_sweep_cost(ref, tgt, pose, K, Ki, L, 0.8)
-        err = (outs[(1, 4)] - want).abs() - RTOL * torch.clamp(want.abs(), min=FLOOR)
-        assert float(err.max()) <= 0.0, float((outs[(1, 4)] - want).abs().max())
+        got = outs[(2, 8, 1)]
+        err = (got - want).abs() - RTOL * torch.clamp(want.abs(), min=FLOOR)
+        assert float(err.max()) <= 0.0, float((got - want).abs().max())
