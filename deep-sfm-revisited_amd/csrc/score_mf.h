@@ -209,6 +209,13 @@ __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, con
     row[32 + 2] = (_Float16)(-1.0f);                             // Ylo = -1 (monomial '1')
     row[48 + 2] = (_Float16)(finite ? -1.0f : 1.0f);             // Yhi = -1 (outlier) / +1 (undecided)
   }
+  // sentinel monomials (zero for every live in-range point): a dead slot
+  // carries kMfSentinel in K = 14 (Ylo = Yhi = -S: a decided outlier), a point
+  // outside the f16 range in K = 15 (Ylo = -S, Yhi = +S: undecided -> float64)
+  row[32 + 14] = (_Float16)(-1.0f);
+  row[32 + 15] = (_Float16)(-1.0f);
+  row[48 + 14] = (_Float16)(-1.0f);
+  row[48 + 15] = (_Float16)(1.0f);
   uint4* out = reinterpret_cast<uint4*>(candF + ((size_t)b * cmax + c) * kMfRec);
   const uint4* in = reinterpret_cast<const uint4*>(row);
 #pragma unroll
@@ -220,9 +227,12 @@ __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, con
 // Monomials in float32 from float32 coordinates (relative error <= 3 * 2^-24
 // against the float64 point, 0.75 * 2^-22 of the 3.75 * 2^-22 representation
 // term of aS), split into f16 hi + lo: m - hi is exact in float32, lo rounds
-// once (2^-22 |m|).  Dead slots are zero; a point past the f16 range (M >
-// 15.9, or NaN) is zeroed and reported (return value).
-__device__ __forceinline__ bool mf_stage_point(const double4 v, bool live, _Float16* frag_tile, int r) {
+// once (2^-22 |m|).  A dead slot (past the span) is zero but for the sentinel
+// K = 14, a point past the f16 range (M > 15.9, or NaN) zero but for K = 15
+// (see k_mf_cands: decided outlier / undecided for every candidate row).
+constexpr float kMfSentinel = 60000.0f;     // exact in f16; +-S dominates every live Ylo / Yhi term
+
+__device__ __forceinline__ void mf_stage_point(const double4 v, bool live, _Float16* frag_tile, int r) {
   const float x = (float)v.x, y = (float)v.y, xp = (float)v.z, yp = (float)v.w;
   float M = fmaxf(fmaxf(fabsf(x), fabsf(y)), fmaxf(fabsf(xp), fabsf(yp)));
   M = fmaxf(M, 1.0f);
@@ -230,7 +240,11 @@ __device__ __forceinline__ bool mf_stage_point(const double4 v, bool live, _Floa
   _Float16 col[48];
 #pragma unroll
   for (int i = 0; i < 48; ++i) col[i] = (_Float16)0.0f;
-  if (live && !bad) {
+  if (!live) {
+    col[32 + 14] = (_Float16)kMfSentinel;
+  } else if (bad) {
+    col[32 + 15] = (_Float16)kMfSentinel;
+  } else {
     const float ma[9] = {xp * x, xp * y, xp, yp * x, yp * y, yp, x, y, 1.0f};
     _Float16 hi[9], lo[9];
 #pragma unroll
@@ -265,7 +279,6 @@ __device__ __forceinline__ bool mf_stage_point(const double4 v, bool live, _Floa
     for (int h = 0; h < 2; ++h)
       *reinterpret_cast<uint4*>(frag_tile + ((size_t)f * 64 + 32 * h + r) * 8) =
           *reinterpret_cast<const uint4*>(col + 16 * f + 8 * h);
-  return bad;
 }
 
 // row of accumulator register g in half h of a 32x32 MFMA output
@@ -312,43 +325,91 @@ extern "C" int sfm_experiment_mf_stamps(unsigned long long* out5, int reset) {
 struct MfAcc {
   mf_float16 a, lo, hi;
 };
+struct MfB {                                                  // one tile's B fragments (ds_read_b128 x 3)
+  mf_half8 b1, b2, bd;
+};
 
-__device__ __forceinline__ MfAcc mf_tile_mfma(const _Float16* frag_tile, int lane, mf_half8 A1, mf_half8 A2,
-                                              mf_half8 AL, mf_half8 AH) {
-  const mf_half8 B1 = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(0 * 64 + lane) * 8);
-  const mf_half8 B2 = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(1 * 64 + lane) * 8);
-  const mf_half8 BD = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(2 * 64 + lane) * 8);
+__device__ __forceinline__ MfB mf_load_b(const _Float16* frag_tile, int lane) {
+  MfB b;
+  b.b1 = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(0 * 64 + lane) * 8);
+  b.b2 = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(1 * 64 + lane) * 8);
+  b.bd = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(2 * 64 + lane) * 8);
+  return b;
+}
+
+__device__ __forceinline__ MfAcc mf_tile_mfma(const MfB& B, mf_half8 A1, mf_half8 A2, mf_half8 AL, mf_half8 AH) {
   mf_float16 z;
 #pragma unroll
   for (int g = 0; g < 16; ++g) z[g] = 0.0f;
   MfAcc r;
-  r.a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B1, z, 0, 0, 0);          // hi x hi (+7 hi x lo) first
-  r.lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(AL, BD, z, 0, 0, 0);
-  r.hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(AH, BD, z, 0, 0, 0);
-  r.a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A2, B2, r.a, 0, 0, 0);        // the small products
+  r.a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B.b1, z, 0, 0, 0);          // hi x hi (+7 hi x lo) first
+  r.lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(AL, B.bd, z, 0, 0, 0);
+  r.hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(AH, B.bd, z, 0, 0, 0);
+  r.a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A2, B.b2, r.a, 0, 0, 0);        // the small products
   return r;
 }
 
-// Decisions of one tile, branch-free: per lane and accumulator register g one
-// packed word acc[g]: the inliers counted so far in bits 0..4 (<= kMfTiles),
-// and bit 5 + t set when the evaluation of tile t was undecided.  (A taken
-// scalar branch per register cost ~10 cycles per instruction overall.)
-// !SAME: separate inlier counts for the num_test / num_ransac_test prefixes.
-template <bool SAME>
-__device__ __forceinline__ void mf_tile_decide(const MfAcc& r, float offs, bool inT, bool inR, uint32_t ubit,
-                                               uint32_t (&acc)[16], int (&cR)[16]) {
+// Decisions of one tile: 4 VALU per evaluation, no scalar masks.
+//   z1 = fl(a^2 - Ylo) (one FMA): inlier  iff a^2 < Ylo  iff sign(z1)
+//   z2 = fl(Yhi - a^2):           outlier iff a^2 > Yhi  iff sign(z2)
+// The FMA rounds once, so the sign of z is the sign of the exact difference
+// (an exact zero is +0 in round-to-nearest: a^2 = Ylo is not an inlier, a^2 =
+// Yhi not an outlier, as the strict compares say); with finite operands (the
+// sentinels replace the old +inf / NaN offsets) no NaN arises.  Each sign bit
+// is shifted into a per-register bit string (v_alignbit: s = s << 1 | z >> 31),
+// so after n tiles bit n-1-t of s1[g] / s2[g] holds tile t's inlier / outlier
+// flag; undecided = neither.
+__device__ __forceinline__ void mf_tile_decide(const MfAcc& r, uint32_t (&s1)[16], uint32_t (&s2)[16]) {
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
-    const float aa = __builtin_fmaf(r.a[g], r.a[g], offs);
-    const bool bin = aa < r.lo[g];
-    const bool bout = aa > r.hi[g];
-    const bool und = !(bin || bout);
-    acc[g] += ((bin && inT) ? 1u : 0u) + (und ? ubit : 0u);
-    if (!SAME) cR[g] += (bin && inR) ? 1 : 0;
+    const float z1 = __builtin_fmaf(r.a[g], r.a[g], -r.lo[g]);
+    const float z2 = __builtin_fmaf(-r.a[g], r.a[g], r.hi[g]);
+    s1[g] = __builtin_amdgcn_alignbit(s1[g], __float_as_uint(z1), 31);
+    s2[g] = __builtin_amdgcn_alignbit(s2[g], __float_as_uint(z2), 31);
   }
 }
 
-static_assert(kMfTiles <= 27 && kMfTiles < 32, "count (5 bits) + one undecided flag per tile in 32 bits");
+// Sum each of 16 per-lane values over the 32 lanes of each wave half by
+// recursive halving (16 lane exchanges instead of 16 x 5).  Afterwards lane
+// L (of its half) holds the sum for g = (L >> 1) & 15, on lanes L and L ^ 1.
+__device__ __forceinline__ int mf_half_reduce(int (&v)[16], int lane) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool b = (lane & 16) != 0;
+    const int recv = __shfl_xor(b ? v[k] : v[k + 8], 16, 64);
+    v[k] = (b ? v[k + 8] : v[k]) + recv;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool b = (lane & 8) != 0;
+    const int recv = __shfl_xor(b ? v[k] : v[k + 4], 8, 64);
+    v[k] = (b ? v[k + 4] : v[k]) + recv;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const bool b = (lane & 4) != 0;
+    const int recv = __shfl_xor(b ? v[k] : v[k + 2], 4, 64);
+    v[k] = (b ? v[k + 2] : v[k]) + recv;
+  }
+  {
+    const bool b = (lane & 2) != 0;
+    const int recv = __shfl_xor(b ? v[0] : v[1], 2, 64);
+    v[0] = (b ? v[1] : v[0]) + recv;
+  }
+  return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ int mf_wave_scan(int x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+static_assert(kMfTiles <= 32, "one bit per tile in 32-bit strings");
 
 template <class Src, bool SAME>
 __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairParams pp, int batch, int cmax,
@@ -360,10 +421,8 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
   __shared__ __attribute__((aligned(16))) _Float16 s_frag[kMfTiles][3][64][8];
   __shared__ double4 s_pts[kMfSpan];
   __shared__ double s_E[kMfWaves][kKC * 10];                 // E (9) + guard Kg of the wave's tile
-  __shared__ uint32_t s_badcol[2][32];                      // bit t of column r: point (t, r) out of range
-                                                            // (by item parity: reset while the other is staged)
   __shared__ uint32_t s_queue[kMfWaves][kMfQueue];
-  __shared__ int32_t s_cnt[kMfWaves][kKC][2];
+  __shared__ int32_t s_cnt[kMfWaves][kKC][2];               // float64 drain counts
   __shared__ int32_t s_first[SFM_MAX_BATCH + 1];
   __shared__ int32_t s_spans[SFM_MAX_BATCH];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -404,10 +463,24 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
     it.p1 = min(max(it.T, it.R), it.p0 + kMfSpan);
     it.c0 = (group * kMfWaves + wv) * kKC;
     it.nc = max(0, min(kKC, cand_total[b] - it.c0));
+    // wave-uniform by construction; say so, so that addresses stay scalar
+    it.b = __builtin_amdgcn_readfirstlane(it.b);
+    it.p0 = __builtin_amdgcn_readfirstlane(it.p0);
+    it.p1 = __builtin_amdgcn_readfirstlane(it.p1);
+    it.c0 = __builtin_amdgcn_readfirstlane(it.c0);
+    it.nc = __builtin_amdgcn_readfirstlane(it.nc);
+    it.T = __builtin_amdgcn_readfirstlane(it.T);
+    it.R = __builtin_amdgcn_readfirstlane(it.R);
     return it;
   };
   constexpr int kPtsPerThread = (kMfSpan + kMfWaves * 64 - 1) / (kMfWaves * 64);
   constexpr int kEPerLane = (kKC * 10 + 63) / 64;
+  int eoff[kEPerLane];                                      // E (9) + Kg of record i / 10: 32-bit offsets
+#pragma unroll
+  for (int j = 0; j < kEPerLane; ++j) {
+    const int i = lane + 64 * j;
+    eoff[j] = (i / 10) * kCandStride + i % 10;
+  }
   double4 pv[kPtsPerThread];
   double ev[kEPerLane];
   mf_half8 nA1, nA2, nAL, nAH;
@@ -418,10 +491,14 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
       const int p = it.p0 + i;
       pv[j] = src.load(it.b, (i < kMfSpan && p < it.p1) ? p : it.p0);
     }
+    if (it.nc > 0) {                                         // uniform; record c0 exists
+      const char* rec0 = reinterpret_cast<const char*>(candE + ((size_t)it.b * cmax + it.c0) * kCandStride);
+      const int lim = it.nc * 10;
 #pragma unroll
-    for (int j = 0; j < kEPerLane; ++j) {
-      const int i = lane + 64 * j;
-      ev[j] = i < it.nc * 10 ? candE[((size_t)it.b * cmax + it.c0 + i / 10) * kCandStride + i % 10] : 0.0;
+      for (int j = 0; j < kEPerLane; ++j) {
+        const unsigned o = lane + 64 * j < lim ? (unsigned)eoff[j] * 8u : 0u;
+        ev[j] = *reinterpret_cast<const double*>(rec0 + o);
+      }
     }
     if (rl < it.nc) {
       const mf_half8* rec = reinterpret_cast<const mf_half8*>(candF + ((size_t)it.b * cmax + it.c0 + rl) * kMfRec);
@@ -434,17 +511,19 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
       for (int j = 0; j < 8; ++j) {
         nA1[j] = (_Float16)0.0f; nA2[j] = (_Float16)0.0f; nAL[j] = (_Float16)0.0f; nAH[j] = (_Float16)0.0f;
       }
-      if (hl == 0) { nAL[2] = (_Float16)(-1.0f); nAH[2] = (_Float16)(-1.0f); }
+      if (hl == 0) {                                         // K = 2: the monomial '1' -> Ylo = Yhi = -1
+        nAL[2] = (_Float16)(-1.0f); nAH[2] = (_Float16)(-1.0f);
+      } else {                                               // K = 14, 15: sentinels -> -S (outlier)
+        nAL[6] = (_Float16)(-1.0f); nAL[7] = (_Float16)(-1.0f);
+        nAH[6] = (_Float16)(-1.0f); nAH[7] = (_Float16)(-1.0f);
+      }
     }
   };
-  if (tid < 64) s_badcol[tid >> 5][tid & 31] = 0u;
-  int par = 0;
   Item cur;
   if (blockIdx.x < total) {
     cur = item_of(blockIdx.x);
     prefetch(cur);
   }
-  __syncthreads();
 #ifdef SFM_MF_STAMPS
   unsigned long long mf_t0_ = __builtin_amdgcn_s_memtime();
   unsigned long long mf_acc_[5] = {0, 0, 0, 0, 0};
@@ -460,8 +539,7 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
       const int i = tid + j * kMfWaves * 64;
       if (i < kMfSpan) {
         s_pts[i] = pv[j];
-        if (mf_stage_point(pv[j], p0 + i < p1, &s_frag[i >> 5][0][0][0], i & 31))
-          atomicOr(&s_badcol[par][i & 31], 1u << (i >> 5));
+        mf_stage_point(pv[j], p0 + i < p1, &s_frag[i >> 5][0][0][0], i & 31);
       }
     }
 #pragma unroll
@@ -471,98 +549,107 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
     }
     const mf_half8 A1 = nA1, A2 = nA2, AL = nAL, AH = nAH;
     __syncthreads();
-    const uint32_t badcol = s_badcol[par][rl];              // bit t: point (t, rl) outside the f16 range
-    // 2. the next item's loads fly while this one computes
-    if (item + (int)gridDim.x < total) {
-      const Item nxt = item_of(item + gridDim.x);
-      prefetch(nxt);
-      cur = nxt;
-    }
+    // 2. the next item's loads fly while this one drains and reduces (issued
+    // after the tile loop: its registers are not live during the MFMAs)
+    auto prefetch_next = [&]() {
+      if (item + (int)gridDim.x < total) {
+        const Item nxt = item_of(item + gridDim.x);
+        prefetch(nxt);
+        cur = nxt;
+      }
+    };
     MF_STAMP(0);
+    if (nc <= 0) prefetch_next();
     if (nc > 0) {
-      uint32_t acc[16];
-      int cR[16];
-#pragma unroll
-      for (int g = 0; g < 16; ++g) { acc[g] = 0u; cR[g] = 0; }
       const int ntiles = (p1 - p0 + 31) >> 5;
-      const int nlive = p1 - p0 - rl;                        // tiles t with 32t < nlive hold a live point here
-      // aa = a*a + offs: 0 for a live point; +inf past the span (a decided
-      // outlier: never counted, never queued); NaN for a point outside the
-      // f16 range (both compares false: undecided -> float64)
-      auto offs_of = [&](int t) {
-        return 32 * t >= nlive ? __builtin_huge_valf() : (((badcol >> t) & 1u) ? __builtin_nanf("") : 0.0f);
-      };
-      // software pipeline, explicit ping-pong (no accumulator copies): the
-      // MFMAs of the next tile run while the current one is decided
-      MfAcc ta = mf_tile_mfma(&s_frag[0][0][0][0], lane, A1, A2, AL, AH), tb;
+      uint32_t s1[16], s2[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) { s1[g] = 0u; s2[g] = 0u; }
+      // software pipeline, explicit ping-pong (no accumulator copies): tile
+      // t + 1's MFMAs run while tile t is decided, and the B fragments of a
+      // tile are read from LDS two tiles ahead of its MFMAs
+      const _Float16* fr = &s_frag[0][0][0][0];
+      constexpr int kTileHalves = 3 * 64 * 8;
+      MfB b0 = mf_load_b(fr, lane), b1 = mf_load_b(fr + (size_t)min(1, ntiles - 1) * kTileHalves, lane);
+      MfAcc ta = mf_tile_mfma(b0, A1, A2, AL, AH), tb;
+      if (ntiles > 2) b0 = mf_load_b(fr + (size_t)2 * kTileHalves, lane);
       for (int t = 0; t < ntiles; t += 2) {
-        if (t + 1 < ntiles) tb = mf_tile_mfma(&s_frag[t + 1][0][0][0], lane, A1, A2, AL, AH);
-        mf_tile_decide<SAME>(ta, offs_of(t), SAME || p0 + 32 * t + rl < T, SAME || p0 + 32 * t + rl < R,
-                             1u << (5 + t), acc, cR);
+        if (t + 1 < ntiles) {
+          tb = mf_tile_mfma(b1, A1, A2, AL, AH);
+          if (t + 3 < ntiles) b1 = mf_load_b(fr + (size_t)(t + 3) * kTileHalves, lane);
+        }
+        mf_tile_decide(ta, s1, s2);
         if (t + 1 >= ntiles) break;
-        if (t + 2 < ntiles) ta = mf_tile_mfma(&s_frag[t + 2][0][0][0], lane, A1, A2, AL, AH);
-        mf_tile_decide<SAME>(tb, offs_of(t + 1), SAME || p0 + 32 * (t + 1) + rl < T,
-                             SAME || p0 + 32 * (t + 1) + rl < R, 1u << (6 + t), acc, cR);
+        if (t + 2 < ntiles) {
+          ta = mf_tile_mfma(b0, A1, A2, AL, AH);
+          if (t + 4 < ntiles) b0 = mf_load_b(fr + (size_t)(t + 4) * kTileHalves, lane);
+        }
+        mf_tile_decide(tb, s1, s2);
       }
       MF_STAMP(1);
-      // the undecided evaluations -> the queue -> float64 (drained whenever it
-      // could overflow: pathological spans may be all undecided)
-      int qn = 0;
+      prefetch_next();
+      // bit n-1-t <-> tile t; dead slots are decided outliers
+      const uint32_t vm = ntiles >= 32 ? ~0u : ((1u << ntiles) - 1u);
+      // 3. the undecided evaluations -> the queue -> float64.  Each lane
+      // writes its own entries at its exclusive prefix; a span with more than
+      // kMfQueue undecided evaluations is drained in several windows.
+      int nl = 0;
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        uint32_t ub = acc[g] >> 5;
-        for (;;) {
-          const uint64_t has = __ballot(ub != 0u);
-          if (!has) break;
-          if (qn > kMfQueue - 64) {
-            wave_sync();
-            mf_drain(sE, s_pts, p0, T, R, kc, lane, cnt, queue, qn);
-            qn = 0;
-            wave_sync();
-          }
-          if (ub) {
-            const int t = __builtin_ctz(ub);
-            ub &= ub - 1u;
-            const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0));
-            queue[pos] = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(p0 + 32 * t + rl);
-          }
-          qn += __popcll(has);
-        }
-      }
-      wave_sync();
-      mf_drain(sE, s_pts, p0, T, R, kc, lane, cnt, queue, qn);
-      MF_STAMP(2);
-      // reduce the per-lane counts over each half's 32 lanes; lane 32h then
-      // holds candidate row mf_row(g, h)'s span count
-      int cT[16];
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        cT[g] = (int)(acc[g] & 31u);
-#pragma unroll
-        for (int d = 16; d >= 1; d >>= 1) {
-          cT[g] += __shfl_xor(cT[g], d, 64);
-          if (!SAME) cR[g] += __shfl_xor(cR[g], d, 64);
-        }
-      }
-      if (rl == 0) {
+      for (int g = 0; g < 16; ++g) nl += __popc(~(s1[g] | s2[g]) & vm);
+      const int incl = mf_wave_scan(nl, lane);
+      const int qtotal = __shfl(incl, 63, 64);
+      for (int base = 0; base < qtotal; base += kMfQueue) {
+        int pos = incl - nl - base;
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-          atomicAdd(&cnt[mf_row(g, hl)][0], cT[g]);
-          atomicAdd(&cnt[mf_row(g, hl)][1], SAME ? cT[g] : cR[g]);
+          uint32_t u = ~(s1[g] | s2[g]) & vm;
+          const uint32_t rowbits = (uint32_t)mf_row(g, hl) << 24;
+          while (u) {
+            const int j = 31 - __clz(u);                     // tiles in ascending order
+            u &= ~(1u << j);
+            if (pos >= 0 && pos < kMfQueue) queue[pos] = rowbits | (uint32_t)(p0 + 32 * (ntiles - 1 - j) + rl);
+            ++pos;
+          }
+        }
+        wave_sync();
+        mf_drain(sE, s_pts, p0, T, R, kc, lane, cnt, queue, min(kMfQueue, qtotal - base));
+        wave_sync();
+      }
+      MF_STAMP(2);
+      // 4. counts: popcounts of the inlier strings (masked to each prefix),
+      // summed over the 32 points of each half, plus the float64 counts
+      int cT[16], cR[16];
+      if (SAME) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) cT[g] = __popc(s1[g]);
+      } else {
+        // tile t holds a point below prefix X iff t < ceil((X - p0 - rl) / 32)
+        auto prefix_mask = [&](int X) {
+          const int tX = min(ntiles, max(0, X - p0 - rl + 31) >> 5);
+          return tX >= 32 ? ~0u : (vm & ~((1u << (ntiles - tX)) - 1u));
+        };
+        const uint32_t mT = prefix_mask(T), mR = prefix_mask(R);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          cT[g] = __popc(s1[g] & mT);
+          cR[g] = __popc(s1[g] & mR);
+        }
+      }
+      const int sumT = mf_half_reduce(cT, lane);
+      const int sumR = SAME ? sumT : mf_half_reduce(cR, lane);
+      if ((lane & 1) == 0) {
+        const int c = mf_row((rl >> 1) & 15, hl);
+        const int dT = sumT + cnt[c][0], dR = sumR + cnt[c][1];
+        cnt[c][0] = 0;
+        cnt[c][1] = 0;
+        if (c < nc) {
+          if (dT) atomicAdd(cntT + (size_t)b * cmax + c0 + c, dT);
+          if (dR) atomicAdd(cntR + (size_t)b * cmax + c0 + c, dR);
         }
       }
       wave_sync();
-      {
-        const int c = lane >> 1, which = lane & 1;
-        const int sc = cnt[c][which];
-        if (c < nc && sc) atomicAdd((which ? cntR : cntT) + (size_t)b * cmax + c0 + c, sc);
-        cnt[c][which] = 0;
-      }
     }
     __syncthreads();                                          // the span is re-staged next item
-    if (tid < 32) s_badcol[par][tid] = 0u;                    // every wave read it before the barrier
-    par ^= 1;
     MF_STAMP(3);
   }
 #ifdef SFM_MF_STAMPS
