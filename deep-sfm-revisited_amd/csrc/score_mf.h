@@ -87,6 +87,13 @@ __device__ __forceinline__ _Float16 f16_up(double v) {
   return (_Float16)(float)(v * (1.0 + 0x1p-10) + 0x1p-24);
 }
 
+// float32 form of f16_up for v >= 0 below the f16 range: v (1 + 2^-10)
+// rounds down by at most 2^-24 relative and the conversion by 2^-11, so the
+// result is >= v; the 2^-24 quantum covers values under the f16 normal range.
+__device__ __forceinline__ _Float16 f16_upf(float v) {
+  return (_Float16)(v * (1.0f + 0x1p-10f) + 0x1p-24f);
+}
+
 // One thread per candidate: the four A rows of its record.
 __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, const double* __restrict__ candE,
                            _Float16* __restrict__ candF, MfParams mp) {
@@ -264,14 +271,17 @@ __device__ __forceinline__ void mf_stage_point(const double4 v, bool live, _Floa
 #pragma unroll
     for (int j = 0; j < 11; ++j) col[32 + j] = (_Float16)md[j];
     // bound monomials, rounded up (>= their float64-point values): M^2 for the
-    // Ylo / Yhi rounding terms, (s1/4)^2 and (s2/4)^2 for the a-error terms
-    const double up = 1.0 + 0x1p-20;
-    const double Mu = (double)M * up;
-    const double s1 = ((double)fabsf(ma[0]) + fabsf(ma[1]) + fabsf(ma[3]) + fabsf(ma[4])) * up * up * 0.25;
-    const double s2 = ((double)fabsf(xp) + fabsf(yp) + fabsf(x) + fabsf(y)) * up * 0.25;
-    col[32 + 11] = f16_up(Mu * Mu);
-    col[32 + 12] = f16_up(s1 * s1);
-    col[32 + 13] = f16_up(s2 * s2);
+    // Ylo / Yhi rounding terms, (s1/4)^2 and (s2/4)^2 for the a-error terms.
+    // In float32: M is within 2^-24 of the float64 point's, each product ma
+    // within 3 * 2^-24, each sum of non-negative terms adds <= 2^-24 per add;
+    // the factors (1 + 2^-19) and (1 + 2^-18) cover that and their own
+    // rounding, f16_upf the squaring and the f16 conversion.
+    const float Mu = M * (1.0f + 0x1p-19f);
+    const float s1 = ((fabsf(ma[0]) + fabsf(ma[1])) + (fabsf(ma[3]) + fabsf(ma[4]))) * (0.25f + 0x1p-20f);
+    const float s2 = ((fabsf(xp) + fabsf(yp)) + (fabsf(x) + fabsf(y))) * (0.25f + 0x1p-20f);
+    col[32 + 11] = f16_upf(Mu * Mu);
+    col[32 + 12] = f16_upf(s1 * s1);
+    col[32 + 13] = f16_upf(s2 * s2);
   }
 #pragma unroll
   for (int f = 0; f < 3; ++f)
@@ -302,15 +312,17 @@ __device__ __forceinline__ void mf_drain(const double* __restrict__ sE, const do
 
 #ifdef SFM_MF_STAMPS
 // experiment builds only (scripts/mf_stamps.py): per-phase wave cycles of
-// k_score_mf: [0] item setup + staging, [1] main loop, [2] queue + float64
-// drain, [3] reduction + atomics + barrier; [4] items (vector atomics only)
-__device__ unsigned long long g_mf_stamps[5];
-extern "C" int sfm_experiment_mf_stamps(unsigned long long* out5, int reset) {
+// k_score_mf: [0] item setup + staging, [1] tile loop, [2] queue build,
+// [3] float64 drain, [4] count reduction + atomics, [5] block barrier,
+// [6] next-item prefetch issue; [7] items (vector atomics only)
+constexpr int kMfStamps = 8;
+__device__ unsigned long long g_mf_stamps[kMfStamps];
+extern "C" int sfm_experiment_mf_stamps(unsigned long long* out, int reset) {
   if (reset) {
-    unsigned long long z[5] = {0, 0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_mf_stamps), z, 40) == hipSuccess ? 0 : 2;
+    unsigned long long z[kMfStamps] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_mf_stamps), z, sizeof(z)) == hipSuccess ? 0 : 2;
   }
-  return hipMemcpyFromSymbol(out5, HIP_SYMBOL(g_mf_stamps), 40) == hipSuccess ? 0 : 2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mf_stamps), kMfStamps * 8) == hipSuccess ? 0 : 2;
 }
 #define MF_STAMP(i)                                                                       \
   do {                                                                                    \
@@ -399,17 +411,32 @@ __device__ __forceinline__ int mf_half_reduce(int (&v)[16], int lane) {
   return v[0] + __shfl_xor(v[0], 1, 64);
 }
 
-// inclusive prefix sum over the 64 lanes
+// inclusive prefix sum over the 64 lanes: Hillis-Steele inside each 16-lane
+// row with DPP row shifts (zero-filled at the row start, VALU speed), then the
+// totals of the preceding rows from three lane reads
 __device__ __forceinline__ int mf_wave_scan(int x, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  return x;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);   // row_shr:8
+  const int r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31);
+  const int r2 = __builtin_amdgcn_readlane(x, 47);
+  const int row = lane >> 4;
+  return x + (row >= 1 ? r0 : 0) + (row >= 2 ? r1 : 0) + (row >= 3 ? r2 : 0);
 }
 
 static_assert(kMfTiles <= 32, "one bit per tile in 32-bit strings");
+
+// Block barrier for LDS reuse only.  __syncthreads() also waits for every
+// outstanding global access of the wave (s_waitcnt vmcnt(0)): here that is
+// the next item's prefetch and the previous item's count atomics, whose
+// latency under load (thousands of cycles) would then be paid at every
+// barrier.  LDS accesses are complete at lgkmcnt(0); register results of the
+// global loads are still waited for where they are used.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 
 template <class Src, bool SAME>
 __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairParams pp, int batch, int cmax,
@@ -424,6 +451,7 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
   __shared__ uint32_t s_queue[kMfWaves][kMfQueue];
   __shared__ int32_t s_cnt[kMfWaves][kKC][2];               // float64 drain counts
   __shared__ int32_t s_first[SFM_MAX_BATCH + 1];
+  __shared__ int32_t s_ctot[SFM_MAX_BATCH];                  // cand_total, read once
   __shared__ int32_t s_spans[SFM_MAX_BATCH];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int hl = lane >> 5, rl = lane & 31;
@@ -435,6 +463,7 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
       const int spans = (max(pp.test[b], pp.rtest[b]) + kMfSpan - 1) / kMfSpan;
       s_spans[b] = spans;
       s_first[b] = acc;
+      s_ctot[b] = cand_total[b];
       acc += groups * spans;
     }
     s_first[batch] = acc;
@@ -449,9 +478,8 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
   // points, A rows and E rows are loaded into registers while the current
   // item computes, so staging costs no global latency
   struct Item { int b, p0, p1, c0, nc, T, R; };
-  auto item_of = [&](int item) {
+  auto item_of = [&](int item, int b) {                       // b: a pair at or before the item's
     Item it;
-    int b = 0;
     while (item >= s_first[b + 1]) ++b;
     const int local = item - s_first[b];
     const int spans = s_spans[b];
@@ -462,7 +490,7 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
     it.p0 = span * kMfSpan;
     it.p1 = min(max(it.T, it.R), it.p0 + kMfSpan);
     it.c0 = (group * kMfWaves + wv) * kKC;
-    it.nc = max(0, min(kKC, cand_total[b] - it.c0));
+    it.nc = max(0, min(kKC, s_ctot[b] - it.c0));
     // wave-uniform by construction; say so, so that addresses stay scalar
     it.b = __builtin_amdgcn_readfirstlane(it.b);
     it.p0 = __builtin_amdgcn_readfirstlane(it.p0);
@@ -475,19 +503,19 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
   };
   constexpr int kPtsPerThread = (kMfSpan + kMfWaves * 64 - 1) / (kMfWaves * 64);
   constexpr int kEPerLane = (kKC * 10 + 63) / 64;
-  int eoff[kEPerLane];                                      // E (9) + Kg of record i / 10: 32-bit offsets
-#pragma unroll
-  for (int j = 0; j < kEPerLane; ++j) {
-    const int i = lane + 64 * j;
-    eoff[j] = (i / 10) * kCandStride + i % 10;
-  }
   double4 pv[kPtsPerThread];
   double ev[kEPerLane];
   mf_half8 nA1, nA2, nAL, nAH;
   auto prefetch = [&](const Item& it) {
+    // an opaque copy of the lane index: the per-lane offsets below are then
+    // recomputed per call instead of being hoisted out of the item loop,
+    // where they would occupy (and spill) registers through the tile loop
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int lh = ln >> 5, lr = ln & 31;
 #pragma unroll
     for (int j = 0; j < kPtsPerThread; ++j) {
-      const int i = tid + j * kMfWaves * 64;
+      const int i = wv * 64 + ln + j * kMfWaves * 64;
       const int p = it.p0 + i;
       pv[j] = src.load(it.b, (i < kMfSpan && p < it.p1) ? p : it.p0);
     }
@@ -495,23 +523,24 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
       const char* rec0 = reinterpret_cast<const char*>(candE + ((size_t)it.b * cmax + it.c0) * kCandStride);
       const int lim = it.nc * 10;
 #pragma unroll
-      for (int j = 0; j < kEPerLane; ++j) {
-        const unsigned o = lane + 64 * j < lim ? (unsigned)eoff[j] * 8u : 0u;
+      for (int j = 0; j < kEPerLane; ++j) {                  // E (9) + Kg of record i / 10
+        const int i = ln + 64 * j;
+        const unsigned o = i < lim ? (unsigned)((i / 10) * kCandStride + i % 10) * 8u : 0u;
         ev[j] = *reinterpret_cast<const double*>(rec0 + o);
       }
     }
-    if (rl < it.nc) {
-      const mf_half8* rec = reinterpret_cast<const mf_half8*>(candF + ((size_t)it.b * cmax + it.c0 + rl) * kMfRec);
-      nA1 = rec[0 + hl];
-      nA2 = rec[2 + hl];
-      nAL = rec[4 + hl];
-      nAH = rec[6 + hl];
+    if (lr < it.nc) {
+      const mf_half8* rec = reinterpret_cast<const mf_half8*>(candF + ((size_t)it.b * cmax + it.c0 + lr) * kMfRec);
+      nA1 = rec[0 + lh];
+      nA2 = rec[2 + lh];
+      nAL = rec[4 + lh];
+      nAH = rec[6 + lh];
     } else {                                                 // absent row: every evaluation a decided outlier
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         nA1[j] = (_Float16)0.0f; nA2[j] = (_Float16)0.0f; nAL[j] = (_Float16)0.0f; nAH[j] = (_Float16)0.0f;
       }
-      if (hl == 0) {                                         // K = 2: the monomial '1' -> Ylo = Yhi = -1
+      if (lh == 0) {                                         // K = 2: the monomial '1' -> Ylo = Yhi = -1
         nAL[2] = (_Float16)(-1.0f); nAH[2] = (_Float16)(-1.0f);
       } else {                                               // K = 14, 15: sentinels -> -S (outlier)
         nAL[6] = (_Float16)(-1.0f); nAL[7] = (_Float16)(-1.0f);
@@ -521,16 +550,16 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
   };
   Item cur;
   if (blockIdx.x < total) {
-    cur = item_of(blockIdx.x);
+    cur = item_of(blockIdx.x, 0);
     prefetch(cur);
   }
 #ifdef SFM_MF_STAMPS
   unsigned long long mf_t0_ = __builtin_amdgcn_s_memtime();
-  unsigned long long mf_acc_[5] = {0, 0, 0, 0, 0};
+  unsigned long long mf_acc_[kMfStamps] = {};
 #endif
   for (int item = blockIdx.x; item < total; item += gridDim.x) {
 #ifdef SFM_MF_STAMPS
-    mf_acc_[4] += 1;
+    mf_acc_[7] += 1;
 #endif
     const int b = cur.b, p0 = cur.p0, p1 = cur.p1, c0 = cur.c0, nc = cur.nc, T = cur.T, R = cur.R;
     // 1. stage the prefetched span (points + B columns) and E rows into LDS
@@ -548,12 +577,12 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
       if (i < kKC * 10) s_E[wv][i] = ev[j];
     }
     const mf_half8 A1 = nA1, A2 = nA2, AL = nAL, AH = nAH;
-    __syncthreads();
+    lds_barrier();
     // 2. the next item's loads fly while this one drains and reduces (issued
     // after the tile loop: its registers are not live during the MFMAs)
     auto prefetch_next = [&]() {
       if (item + (int)gridDim.x < total) {
-        const Item nxt = item_of(item + gridDim.x);
+        const Item nxt = item_of(item + gridDim.x, cur.b);   // items rise monotonically
         prefetch(nxt);
         cur = nxt;
       }
@@ -588,6 +617,7 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
       }
       MF_STAMP(1);
       prefetch_next();
+      MF_STAMP(6);
       // bit n-1-t <-> tile t; dead slots are decided outliers
       const uint32_t vm = ntiles >= 32 ? ~0u : ((1u << ntiles) - 1u);
       // 3. the undecided evaluations -> the queue -> float64.  Each lane
@@ -597,23 +627,28 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
 #pragma unroll
       for (int g = 0; g < 16; ++g) nl += __popc(~(s1[g] | s2[g]) & vm);
       const int incl = mf_wave_scan(nl, lane);
-      const int qtotal = __shfl(incl, 63, 64);
+      const int qtotal = __builtin_amdgcn_readlane(incl, 63);
       for (int base = 0; base < qtotal; base += kMfQueue) {
         int pos = incl - nl - base;
+        uint32_t ub[16];
+#pragma unroll
+        for (int g = 0; g < 16; ++g) ub[g] = ~(s1[g] | s2[g]) & vm;
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-          uint32_t u = ~(s1[g] | s2[g]) & vm;
+          uint32_t u = ub[g];
           const uint32_t rowbits = (uint32_t)mf_row(g, hl) << 24;
           while (u) {
-            const int j = 31 - __clz(u);                     // tiles in ascending order
+            const int j = 31 - __clz(u);
             u &= ~(1u << j);
             if (pos >= 0 && pos < kMfQueue) queue[pos] = rowbits | (uint32_t)(p0 + 32 * (ntiles - 1 - j) + rl);
             ++pos;
           }
         }
         wave_sync();
+        MF_STAMP(2);
         mf_drain(sE, s_pts, p0, T, R, kc, lane, cnt, queue, min(kMfQueue, qtotal - base));
         wave_sync();
+        MF_STAMP(3);
       }
       MF_STAMP(2);
       // 4. counts: popcounts of the inlier strings (masked to each prefix),
@@ -648,12 +683,13 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
         }
       }
       wave_sync();
+      MF_STAMP(4);
     }
-    __syncthreads();                                          // the span is re-staged next item
-    MF_STAMP(3);
+    lds_barrier();                                            // the span is re-staged next item
+    MF_STAMP(5);
   }
 #ifdef SFM_MF_STAMPS
   if (lane == 0)
-    for (int i = 0; i < 5; ++i) atomicAdd(&g_mf_stamps[i], mf_acc_[i]);
+    for (int i = 0; i < kMfStamps; ++i) atomicAdd(&g_mf_stamps[i], mf_acc_[i]);
 #endif
 }

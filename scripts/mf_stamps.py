@@ -11,14 +11,14 @@ flow, K, _, _ = synth.kitti_pair_batch(8, seed=1000, device=dev)
 hp = TwoViewHotPath(8, (376, 1242), (94, 311), 32, 128, 8, 1e-4, 1.0, True, 0.6, device=dev)
 hp.pose(flow, K); torch.cuda.synchronize()
 lib = _lib.load()
-out = (ctypes.c_ulonglong * 5)()
+out = (ctypes.c_ulonglong * 8)()
 lib.sfm_experiment_mf_stamps(out, 1)
 _lib.profile_reset(); _lib.profile_enable(True)
 hp.pose(flow, K); torch.cuda.synchronize(); _lib.profile_enable(False)
 ms, n = _lib.profile_read("ransac_score")
 lib.sfm_experiment_mf_stamps(out, 0)
-tot = sum(out[:4])
-names = ["setup+staging", "main loop", "queue+drain", "reduce+atomics+barrier"]
-print("score %.3f ms, items %d" % (ms, out[4]))
+names = ["setup+staging", "tile loop", "queue build", "float64 drain", "reduce+atomics", "block barrier", "prefetch issue"]
+tot = sum(out[:len(names)])
+print("score %.3f ms, items %d" % (ms, out[7]))
 for i, nm in enumerate(names):
-    print("%-24s %6.1f %%  %.0f cycles/item/wave" % (nm, 100.0 * out[i] / tot, out[i] / max(out[4], 1)))
+    print("%-24s %6.1f %%  %.0f cycles/item/wave" % (nm, 100.0 * out[i] / tot, out[i] / max(out[7], 1)))
