@@ -22,7 +22,9 @@ across ranks with no data-path collective ("scaling": "weak"); RCCL only for
 the barrier, the max-over-ranks timing reduction and the device-name gather.
 
 Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel (RANSAC
-scoring, fp32 VALU); `roofline_sweep` the HBM-bound cost-volume kernel; both
+scoring: k_score_mf on the f16 matrix cores, or k_score32 on the fp32 VALU
+when the matrix-core scorer is off); `roofline_sweep` the HBM-bound
+cost-volume kernel; both
 average launch durations come from HIP events recorded by libsfm_hip around
 every launch on the launching stream during the timed region; `traffic` is
 the PMC-measured HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE, gfx950
@@ -44,7 +46,9 @@ PEAK_HBM_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_FP64_TFLOPS = 78.6      # MI355X fp64 vector spec
 PEAK_FP32_TFLOPS = 157.3     # MI355X fp32 vector spec (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0    # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+PEAK_F16_TFLOPS = 2500.0     # MI355X dense f16 MFMA (same rate as bf16; no sparsity)
 FLOP_PER_EVAL = 50           # Ex, xE, x'Ex, sqrt, div, |.|
+MF_MFMA_FLOP_PER_EVAL = 128  # k_score_mf: 4 x v_mfma_f32_32x32x16_f16 (32768 FLOP each) per 32x32 evaluations
 
 # name -> (pairs per GPU, image hw, ransac_iter, nlabel, cost dtype, sparse keypoints per pair)
 CONFIGS = {
@@ -107,6 +111,27 @@ def pmc_traffic(args):
                 (args.config, args.batch, args.nlabel, args.iters, args.cost_dtype):
             return {n: v.get("hbm_bytes") for n, v in d["kernels"].items()}, os.path.relpath(f, ROOT)
     return {}, None
+
+
+def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, traffic_src):
+    """Roofline line of the RANSAC scoring kernel.  achieved = the algorithmic
+    rate (SURVEY §8d: 50 FLOP per (candidate E, correspondence) evaluation);
+    peak = the unit that executes it: the dense f16 MFMA peak for k_score_mf
+    (exact decisions from split-f16 matrix-core products, csrc/score_mf.h), the
+    fp32 VALU peak for k_score32.  For k_score_mf `mfma_issued` is the MFMA
+    pipe's own utilisation (4 MFMAs per 1024 evaluations): the kernel's floor."""
+    work = (f"{done} evals x {FLOP_PER_EVAL} FLOP per launch: {cands} candidate E x N={n} = {evals}, "
+            f"minus {skipped} skipped by exact bound pruning ({100.0 * skipped / max(evals, 1):.1f}%)")
+    if use_mf:
+        issued = evals * MF_MFMA_FLOP_PER_EVAL / (ms * 1e-3) / 1e12
+        return {"kernel": "ransac_score (k_score_mf)", "bound": "mfma-f16", "achieved": round(tflops, 3),
+                "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_F16_TFLOPS, 4),
+                "mfma_issued": {"flop_per_eval": MF_MFMA_FLOP_PER_EVAL, "tflops": round(issued, 1),
+                                "frac": round(issued / PEAK_F16_TFLOPS, 4)},
+                "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work}
+    return {"kernel": "ransac_score (k_score32)", "bound": "valu-fp32", "achieved": round(tflops, 3),
+            "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
+            "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work}
 
 
 def cpu_info(threads):
@@ -307,6 +332,8 @@ def _main_gpu(args, dist):
     done = evals - skipped                          # evaluations the launch performed
     score_ms = kt["ransac_score"]
     score_tflops = done * FLOP_PER_EVAL / (score_ms * 1e-3) / 1e12
+    use_mf = bool(_lib.tune_get("score_mf")) and not _lib.tune_get("score_mfma") and \
+        2.0 ** -15 <= args.threshold < 1.0
     h, w = fhw
     s = 4 if cost_dtype == torch.float32 else 2
     sweep_bytes = B * (2 * C * args.nlabel * h * w * s + 2 * C * h * w * 4)
@@ -339,15 +366,8 @@ def _main_gpu(args, dist):
             "dist": {"world_size": torch.distributed.get_world_size() if world > 1 else 1,
                      "backend": torch.distributed.get_backend() if world > 1 else None,
                      "devices": names},
-            # k_score32 decides ~99% of evaluations in float32 (the rest re-tested in
-            # float64), so the binding peak is the float32 VALU one
-            "roofline": {"kernel": "ransac_score", "bound": "valu-fp32", "achieved": round(score_tflops, 3),
-                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(score_tflops / PEAK_FP32_TFLOPS, 4),
-                         "traffic": traffic.get("ransac_score"), "traffic_source": traffic_src,
-                         "avg_launch_ms": round(score_ms, 4),
-                         "work": (f"{done} evals x {FLOP_PER_EVAL} FLOP per launch: {sum(cands)} candidate E x "
-                                  f"N={hp.n} = {evals}, minus {skipped} skipped by exact bound pruning "
-                                  f"({100.0 * skipped / max(evals, 1):.1f}%)")},
+            "roofline": score_roofline(use_mf, score_tflops, done, evals, skipped, sum(cands), hp.n, score_ms,
+                                       traffic.get("ransac_score"), traffic_src),
             "roofline_sweep": {"kernel": "plane_sweep", "bound": "hbm", "achieved": round(sweep_gbs, 1),
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(sweep_gbs / PEAK_HBM_GBS, 4),
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,

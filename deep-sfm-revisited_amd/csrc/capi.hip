@@ -82,28 +82,57 @@ int sfm_abi_version(void) { return SFM_ABI_VERSION; }
 
 const char* sfm_last_error(void) { return sfm::g_error.c_str(); }
 
+namespace {
+// every tuning key: its field and accepted values
+struct TuneKey {
+  const char* name;
+  int sfm::Tuning::*field;
+  bool (*ok)(int);
+};
+bool v_1_64(int v) { return v >= 1 && v <= 64; }
+bool v_01(int v) { return v == 0 || v == 1; }
+const TuneKey kTuneKeys[] = {
+    {"solve_lanes", &sfm::Tuning::solve_lanes, v_1_64},
+    {"roots_lanes", &sfm::Tuning::roots_lanes, v_1_64},
+    {"sweep_lane_pixels", &sfm::Tuning::sweep_lane_pixels, [](int v) { return v >= 0 && v <= 2; }},
+    {"sweep_items_per_block", &sfm::Tuning::sweep_items_per_block,
+     [](int v) { return v == 1 || v == 2 || v == 4 || v == 8; }},
+    {"sweep_flat", &sfm::Tuning::sweep_flat, [](int v) { return v >= 0 && v <= 2; }},
+    {"sweep_nj", &sfm::Tuning::sweep_nj, [](int v) { return v == 1 || v == 2 || v == 4; }},
+    {"sweep_group", &sfm::Tuning::sweep_group, [](int v) { return v == 4 || v == 8; }},
+    {"score_blocks_per_cu", &sfm::Tuning::score_blocks_per_cu, v_1_64},
+    {"score_fp32", &sfm::Tuning::score_fp32, v_01},
+    {"score_prune", &sfm::Tuning::score_prune, v_01},
+    {"score_mfma", &sfm::Tuning::score_mfma, v_01},
+    {"score_mf", &sfm::Tuning::score_mf, v_01},
+    {"score_mf_blocks_per_cu", &sfm::Tuning::score_mf_blocks_per_cu, [](int v) { return v >= 1 && v <= 8; }},
+    {"score_interleave", &sfm::Tuning::score_interleave, v_01},
+    {"conv_rolling", &sfm::Tuning::conv_rolling, v_01},
+    {"score_precision", &sfm::Tuning::score_precision, [](int v) { return v == 64 || v == 32 || v == 16; }},
+};
+const TuneKey* find_key(const char* key) {
+  for (const TuneKey& k : kTuneKeys)
+    if (std::string(key) == k.name) return &k;
+  return nullptr;
+}
+}  // namespace
+
 int sfm_tune_set(const char* key, int value) {
   if (!key) { sfm::set_error("sfm_tune_set: null key"); return SFM_ERR_ARG; }
-  const std::string k(key);
-  sfm::Tuning& t = sfm::tuning();
-  if (k == "solve_lanes" && value >= 1 && value <= 64) t.solve_lanes = value;
-  else if (k == "roots_lanes" && value >= 1 && value <= 64) t.roots_lanes = value;
-  else if (k == "sweep_lane_pixels" && value >= 0 && value <= 2) t.sweep_lane_pixels = value;
-  else if (k == "sweep_items_per_block" && (value == 1 || value == 2 || value == 4 || value == 8))
-    t.sweep_items_per_block = value;
-  else if (k == "sweep_flat" && value >= 0 && value <= 2) t.sweep_flat = value;
-  else if (k == "sweep_nj" && (value == 1 || value == 2 || value == 4)) t.sweep_nj = value;
-  else if (k == "sweep_group" && (value == 4 || value == 8)) t.sweep_group = value;
-  else if (k == "score_blocks_per_cu" && value >= 1 && value <= 64) t.score_blocks_per_cu = value;
-  else if (k == "score_fp32" && (value == 0 || value == 1)) t.score_fp32 = value;
-  else if (k == "score_prune" && (value == 0 || value == 1)) t.score_prune = value;
-  else if (k == "score_mfma" && (value == 0 || value == 1)) t.score_mfma = value;
-  else if (k == "score_mf" && (value == 0 || value == 1)) t.score_mf = value;
-  else if (k == "score_mf_blocks_per_cu" && value >= 1 && value <= 8) t.score_mf_blocks_per_cu = value;
-  else if (k == "score_interleave" && (value == 0 || value == 1)) t.score_interleave = value;
-  else if (k == "conv_rolling" && (value == 0 || value == 1)) t.conv_rolling = value;
-  else if (k == "score_precision" && (value == 64 || value == 32 || value == 16)) t.score_precision = value;
-  else { sfm::set_error("sfm_tune_set: unknown key or value out of range: " + k); return SFM_ERR_ARG; }
+  const TuneKey* k = find_key(key);
+  if (!k || !k->ok(value)) {
+    sfm::set_error("sfm_tune_set: unknown key or value out of range: " + std::string(key));
+    return SFM_ERR_ARG;
+  }
+  sfm::tuning().*(k->field) = value;
+  return SFM_OK;
+}
+
+int sfm_tune_get(const char* key, int* value) {
+  if (!key || !value) { sfm::set_error("sfm_tune_get: null argument"); return SFM_ERR_ARG; }
+  const TuneKey* k = find_key(key);
+  if (!k) { sfm::set_error("sfm_tune_get: unknown key: " + std::string(key)); return SFM_ERR_ARG; }
+  *value = sfm::tuning().*(k->field);
   return SFM_OK;
 }
 

@@ -53,10 +53,10 @@
 typedef _Float16 mf_half8 __attribute__((ext_vector_type(8)));
 typedef float mf_float16 __attribute__((ext_vector_type(16)));
 
-constexpr int kMfWaves = 8;                 // waves per block: one 32-candidate tile each
+constexpr int kMfWaves = 12;                // waves per block (3 per SIMD): one 32-candidate tile each
 constexpr int kMfSpan = 768;                // points per item (B fragments staged in LDS)
 constexpr int kMfTiles = kMfSpan / 32;
-constexpr int kMfQueue = 1024;              // undecided entries per wave (drained when it could overflow)
+constexpr int kMfQueue = 256;               // undecided entries per wave (drained in windows of this size)
 constexpr int kMfRec = 64;                  // f16 per candidate: 4 A rows of K = 16
 constexpr float kMfMaxM = 15.9f;            // M^4 stays below the f16 maximum
 
@@ -439,7 +439,7 @@ __device__ __forceinline__ void lds_barrier() {
 
 
 template <class Src, bool SAME>
-__global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairParams pp, int batch, int cmax,
+__global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(kMfWaves / 4, kMfWaves / 4))) void k_score_mf(const Src src, PairParams pp, int batch, int cmax,
                                                            const int32_t* __restrict__ cand_total,
                                                            const double* __restrict__ candE,
                                                            const _Float16* __restrict__ candF,
@@ -594,26 +594,18 @@ __global__ __launch_bounds__(kMfWaves * 64) void k_score_mf(const Src src, PairP
       uint32_t s1[16], s2[16];
 #pragma unroll
       for (int g = 0; g < 16; ++g) { s1[g] = 0u; s2[g] = 0u; }
-      // software pipeline, explicit ping-pong (no accumulator copies): tile
-      // t + 1's MFMAs run while tile t is decided, and the B fragments of a
-      // tile are read from LDS two tiles ahead of its MFMAs
+      // 168 VGPRs, three waves per SIMD: the MFMA and LDS latencies of one
+      // wave's tile are covered by the other two (measured 5 % faster than two
+      // waves per SIMD with a ping-pong of two accumulator sets, 256 VGPRs)
       const _Float16* fr = &s_frag[0][0][0][0];
       constexpr int kTileHalves = 3 * 64 * 8;
-      MfB b0 = mf_load_b(fr, lane), b1 = mf_load_b(fr + (size_t)min(1, ntiles - 1) * kTileHalves, lane);
-      MfAcc ta = mf_tile_mfma(b0, A1, A2, AL, AH), tb;
-      if (ntiles > 2) b0 = mf_load_b(fr + (size_t)2 * kTileHalves, lane);
-      for (int t = 0; t < ntiles; t += 2) {
-        if (t + 1 < ntiles) {
-          tb = mf_tile_mfma(b1, A1, A2, AL, AH);
-          if (t + 3 < ntiles) b1 = mf_load_b(fr + (size_t)(t + 3) * kTileHalves, lane);
-        }
-        mf_tile_decide(ta, s1, s2);
-        if (t + 1 >= ntiles) break;
-        if (t + 2 < ntiles) {
-          ta = mf_tile_mfma(b0, A1, A2, AL, AH);
-          if (t + 4 < ntiles) b0 = mf_load_b(fr + (size_t)(t + 4) * kTileHalves, lane);
-        }
-        mf_tile_decide(tb, s1, s2);
+      // three waves per SIMD: one accumulator set, the B fragments one tile ahead
+      MfB bn = mf_load_b(fr, lane);
+      for (int t = 0; t < ntiles; ++t) {
+        const MfB bc = bn;
+        if (t + 1 < ntiles) bn = mf_load_b(fr + (size_t)(t + 1) * kTileHalves, lane);
+        const MfAcc r = mf_tile_mfma(bc, A1, A2, AL, AH);
+        mf_tile_decide(r, s1, s2);
       }
       MF_STAMP(1);
       prefetch_next();

@@ -76,6 +76,7 @@ _SIGS = [
     ("sfm_to_channels_last_bf16", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp]),
     ("sfm_tune_set", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    ("sfm_tune_get", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     ("sfm_profile_enable", ctypes.c_int, [ctypes.c_int]),
     ("sfm_profile_reset", ctypes.c_int, []),
     ("sfm_profile_read", ctypes.c_int,
@@ -154,3 +155,10 @@ def profile_read(name):
 def tune(key, value):
     """Set a launch-shape knob of libsfm_hip (see sfm_tune_set in include/sfm_hip.h)."""
     check(load().sfm_tune_set(key.encode(), int(value)), "sfm_tune_set")
+
+
+def tune_get(key):
+    """The current value of a tuning knob (sfm_tune_get)."""
+    v = ctypes.c_int(0)
+    check(load().sfm_tune_get(key.encode(), ctypes.byref(v)), "sfm_tune_get")
+    return v.value

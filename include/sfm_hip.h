@@ -280,35 +280,42 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
 int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
                               void* stream);
 
-/* Tuning knobs (process-wide; every key and its accepted values):
+/* Tuning knobs (process-wide; every key, its accepted values and default):
  *
  *   launch shape only -- outputs are bit-identical for every value:
  *     "solve_lanes"           1..64   lanes per wave in k_solve_front (32)
- *     "roots_lanes"           1..64   lanes per wave in k_roots
- *     "sweep_lane_pixels"     0..2    pixel-to-lane mapping of the per-row sweep
- *     "sweep_items_per_block" 1,2,4,8 sweep work items per block (4)
- *     "sweep_group"           4, 8    rows per sweep slab window
- *     "score_blocks_per_cu"   1..64   persistent score blocks per CU (32)
- *     "score_prune"           0, 1    exact bound pruning (1; winner, count, E, P
- *                                     unchanged -- losing hypotheses' scores
- *                                     become lower bounds, so it is off whenever
- *                                     per-hypothesis scores are requested)
- *     "score_interleave"      0, 1    pair-interleaved score items (0)
- *     "score_fp32"            0, 1    float32 pre-decision level (1; exact by proof)
- *     "score_mfma"            0, 1    matrix-core scorer (0; exact, slower)
+ *     "roots_lanes"           1..64   lanes per wave in k_roots (32)
+ *     "sweep_lane_pixels"     0..2    pixel-to-lane mapping of the per-row sweep (0)
+ *     "sweep_items_per_block" 1,2,4,8 work items per block of the per-row sweep (4)
+ *     "sweep_nj"              1,2,4   pixels per lane of k_sweep_tile (1; bf16 uses 2)
+ *     "score_blocks_per_cu"   1..64   persistent k_score32 blocks per CU (32)
+ *     "score_mf_blocks_per_cu" 1..8   persistent k_score_mf blocks per CU (1)
+ *     "score_prune"           0, 1    exact bound pruning in k_score32 (1; winner,
+ *                                     count, E, P unchanged -- losing hypotheses'
+ *                                     scores become lower bounds, so it is off
+ *                                     whenever per-hypothesis scores are requested)
+ *     "score_interleave"      0, 1    pair-interleaved k_score32 items (0)
+ *     "score_fp32"            0, 1    float32 pre-decision level of k_score32 (1; exact by proof)
+ *     "score_mf"              0, 1    split-f16 matrix-core scorer k_score_mf (1; exact by proof)
+ *     "score_mfma"            0, 1    f32 matrix-core scorer k_score_mx (0; exact, slower)
  *     "conv_rolling"          0, 1    rolling-plane Conv3d for cin 32 (1; same bits)
  *
- *   results MAY change:
- *     "sweep_flat"            0, 1    1 (default): the single-launch sweep, whose
- *                                     4-tap sum uses FMA (differs from the
- *                                     per-row kernel's reference order by
- *                                     <= 7.2e-7 absolute on N(0,1) features);
- *                                     0: per-row kernel in reference order
+ *   results MAY change (sweep outputs by FMA rounding only):
+ *     "sweep_flat"            0, 1, 2 2 (default): k_sweep_tile, 1: k_sweep_flat
+ *                                     (the two are bit-identical); both sum the
+ *                                     four bilinear taps with FMA, which differs
+ *                                     from 0, the per-row kernel in the
+ *                                     reference's mul/add order, by <= 7.2e-7
+ *                                     absolute on N(0,1) features
+ *     "sweep_group"           4, 8    channels per sweep window (8); the channel
+ *                                     group changes nothing but the launch shape
  *     "score_precision"       64, 32, 16  64 (default): the reference's float64
  *                                     ComputeError decision, exact; 32 / 16:
  *                                     ComputeError<float> / <half> semantics
  *                                     (approximate inlier sets, BASELINE C5) */
 int sfm_tune_set(const char* key, int value);
+/* The current value of a tuning key. */
+int sfm_tune_get(const char* key, int* value);
 
 /* ------------------------------------------------------------------------
  * Per-kernel timing (HIP events recorded around every launch on the

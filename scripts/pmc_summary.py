@@ -8,7 +8,7 @@ bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is taken as is
 algorithmic byte count of the volume to 0.2%).  Infinity-Cache hits are
 counted in FETCH_SIZE, so re-reads of L3-resident inputs show up there.
 
-usage: python scripts/pmc_summary.py gpurun_out/pmc profiles/r01_pmc.json
+usage: python scripts/pmc_summary.py gpurun_out/pmc profiles/r02_pmc_v1.json
 """
 import collections
 import csv
@@ -23,6 +23,10 @@ KERNELS = {"k_sweep_flat": "plane_sweep", "k_score32": "ransac_score", "k_score"
 
 
 def kernel_key(name):
+    if "k_score_mf" in name or "k_mf_cands" in name:   # mangled names in the rocprof CSV
+        return "ransac_score"
+    if "k_sweep_tile" in name:
+        return "plane_sweep"
     base = name.split("(")[0]
     for k, v in KERNELS.items():     # k_score32 is checked before k_score
         if base.endswith("::" + k) or ("::" + k + "<") in base:

@@ -136,3 +136,27 @@ def test_regularisation_and_flow2depth_validate_arguments():
     # flow2depth: empty image
     assert lib.sfm_flow2depth(v, v, v, 1, 0, 10, o, None) == 1
     assert lib.sfm_tune_set(b"conv_rolling", 2) == 1
+
+
+def test_tuning_keys_round_trip():
+    """Every key the header documents can be read back; set values stick;
+    out-of-range values are refused and leave the key unchanged."""
+    import re
+    from sfm_amd import _lib
+    doc = open(os.path.join(ROOT, "include", "sfm_hip.h")).read()
+    block = doc[doc.index("Tuning knobs"):doc.index("int sfm_tune_set")]
+    keys = re.findall(r'"([a-z0-9_]+)"', block)
+    assert len(set(keys)) == 16 and "score_mf" in keys and "sweep_nj" in keys
+    for k in keys:
+        _lib.tune_get(k)
+    old = _lib.tune_get("sweep_nj")
+    try:
+        _lib.tune("sweep_nj", 4)
+        assert _lib.tune_get("sweep_nj") == 4
+        with pytest.raises(Exception):
+            _lib.tune("sweep_nj", 3)
+        assert _lib.tune_get("sweep_nj") == 4
+    finally:
+        _lib.tune("sweep_nj", old)
+    with pytest.raises(Exception):
+        _lib.tune_get("no_such_knob")
