@@ -649,8 +649,29 @@ __device__ __forceinline__ void sign_step(const SturmR& S, double a, double& lf,
   }
 }
 
+#ifdef SFM_ROOTS_STATS
+// experiment builds only (scripts/roots_stats.py): Sturm-sequence evaluations
+// and falsi steps per k_roots thread, indexed by (block, thread)
+__device__ unsigned int g_roots_evals[1 << 17];
+__device__ unsigned int g_roots_falsi[1 << 17];
+#define ROOTS_COUNT(arr) \
+  (++arr[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x])
+__device__ unsigned long long g_roots_phase[4][1 << 17];   // cycles: scale, build, bracket, isolate
+#define ROOTS_PHASE(i, t0)                                                                         \
+  do {                                                                                             \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime();                                   \
+    g_roots_phase[i][((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x] +=   \
+        t1_ - t0;                                                                                  \
+    t0 = t1_;                                                                                      \
+  } while (0)
+#else
+#define ROOTS_PHASE(i, t0) ((void)0)
+#define ROOTS_COUNT(arr) ((void)0)
+#endif
+
 // numchanges (sturm.cu:369-385)
 __device__ __forceinline__ int sign_changes_r(const SturmR& S, double a) {
+  ROOTS_COUNT(g_roots_evals);
   int ch = 0;
   double lf = horner_r<0>(S, a);
   sign_step<1>(S, a, lf, ch); sign_step<2>(S, a, lf, ch); sign_step<3>(S, a, lf, ch);
@@ -660,8 +681,11 @@ __device__ __forceinline__ int sign_changes_r(const SturmR& S, double a) {
   return ch;
 }
 
-// modrf_pos (sturm.cu:43-207) on the register copy of s[0]
-__device__ int falsi_r(const SturmR& S, double a, double b, double* val, bool inv) {
+// modrf_pos (sturm.cu:43-207) on the register copy of s[0].  This and the
+// functions below are force-inlined: a SturmR passed by reference to an
+// outlined call has to live in memory (scratch), and every Horner step of
+// the isolation then waited on it (95 % of k_roots' time).
+__device__ __forceinline__ int falsi_r(const SturmR& S, double a, double b, double* val, bool inv) {
   const double* c = S.c;   // s[0] occupies c[0..10]
   if (inv) { double t = a; a = 1.0 / b; b = 1.0 / t; }
   double fa, fb;
@@ -679,6 +703,7 @@ __device__ int falsi_r(const SturmR& S, double a, double b, double* val, bool in
   if (fabs(fb) < kRelErr) { *val = inv ? 1.0 / b : b; return 1; }
   double lfx = fa;
   for (int it = 0; it < kMaxIt; ++it) {
+    ROOTS_COUNT(g_roots_falsi);
     const double x = (fb * a - fa * b) / (fb - fa);
     double fx;
     if (inv) {
@@ -700,47 +725,80 @@ __device__ int falsi_r(const SturmR& S, double a, double b, double* val, bool in
   return 0;
 }
 
-// modrf (sturm.cu:218-275), leading coefficient omitted at +-1 as in the reference
-__device__ int falsi_any_r(const SturmR& S, double a, double b, double* val) {
+// modrf (sturm.cu:218-275), leading coefficient omitted at +-1 as in the
+// reference; the case analysis picks (a, b, inverted) for one falsi_r call
+__device__ __forceinline__ int falsi_any_r(const SturmR& S, double a, double b, double* val) {
   const double* c = S.c;
   if (a > b) { double t = a; a = b; b = t; }
-  if (b <= 1.0 && a >= -1.0) return falsi_r(S, a, b, val, false);
-  if (a >= 1.0 || b <= -1.0) return falsi_r(S, a, b, val, true);
-  double fp1 = 0.0, fm1 = 0.0, fa = 0.0, fb = 0.0;
+  bool inv;
+  if (b <= 1.0 && a >= -1.0) {
+    inv = false;
+  } else if (a >= 1.0 || b <= -1.0) {
+    inv = true;
+  } else {
+    double fp1 = 0.0, fm1 = 0.0, fa = 0.0, fb = 0.0;
 #pragma unroll
-  for (int i = 9; i >= 0; --i) {
-    fp1 = c[i] + fp1;
-    fm1 = c[i] - fm1;
-    fa = a * fa + c[i];
-    fb = b * fb + c[i];
+    for (int i = 9; i >= 0; --i) {
+      fp1 = c[i] + fp1;
+      fm1 = c[i] - fm1;
+      fa = a * fa + c[i];
+      fb = b * fb + c[i];
+    }
+    if (a < -1.0 && b > 1.0) {
+      if (fa * fm1 < 0.0) { b = -1.0; inv = true; }
+      else if (fb * fp1 < 0.0) { a = 1.0; inv = true; }
+      else { a = -1.0; b = 1.0; inv = false; }
+    } else if (a < -1.0) {
+      if (fa * fm1 < 0.0) { b = -1.0; inv = true; }
+      else { a = -1.0; inv = false; }
+    } else {
+      if (fb * fp1 < 0.0) { a = 1.0; inv = true; }
+      else { b = 1.0; inv = false; }
+    }
   }
-  if (a < -1.0 && b > 1.0) {
-    if (fa * fm1 < 0.0) return falsi_r(S, a, -1.0, val, true);
-    if (fb * fp1 < 0.0) return falsi_r(S, 1.0, b, val, true);
-    return falsi_r(S, -1.0, 1.0, val, false);
+  return falsi_r(S, a, b, val, inv);
+}
+
+// Work stack of isolate_r in LDS, one column per lane (stride kStkLanes), so
+// that pushes and pops cost an LDS round trip instead of a scratch one.
+constexpr int kStkDepth = 24;
+constexpr int kStkLanes = 32;
+struct IsoStack {
+  double* lohi;   // [kStkDepth][2][kStkLanes] + lane
+  int* ints;      // [kStkDepth][4][kStkLanes] + lane
+  __device__ __forceinline__ void put(int i, double lo, double hi, int atlo, int athi, int off, int depth) const {
+    lohi[(2 * i) * kStkLanes] = lo;
+    lohi[(2 * i + 1) * kStkLanes] = hi;
+    ints[(4 * i) * kStkLanes] = atlo;
+    ints[(4 * i + 1) * kStkLanes] = athi;
+    ints[(4 * i + 2) * kStkLanes] = off;
+    ints[(4 * i + 3) * kStkLanes] = depth;
   }
-  if (a < -1.0) {
-    if (fa * fm1 < 0.0) return falsi_r(S, a, -1.0, val, true);
-    return falsi_r(S, -1.0, b, val, false);
-  }
-  if (fb * fp1 < 0.0) return falsi_r(S, 1.0, b, val, true);
-  return falsi_r(S, a, 1.0, val, false);
+};
+
+// roots[off] = v with static indices (a dynamic index would put roots in scratch)
+__device__ __forceinline__ void put_root(double roots[10], int off, double v) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+    if (i == off) roots[i] = v;
 }
 
 // sbisect<depth> (sturm.cu:450-555) as an explicit depth-first work stack
-__device__ void isolate_r(const SturmR& S, double lo, double hi, int atlo, int athi, double roots[10]) {
-  struct Iv { double lo, hi; int atlo, athi, off, depth; };
-  Iv stk[24];
+__device__ __forceinline__ void isolate_r(const SturmR& S, double lo, double hi, int atlo, int athi, double roots[10],
+                                          const IsoStack& stk) {
   int sp = 0;
-  stk[sp++] = Iv{lo, hi, atlo, athi, 0, 0};
+  stk.put(sp++, lo, hi, atlo, athi, 0, 0);
   while (sp > 0) {
-    const Iv iv = stk[--sp];
-    if (iv.depth >= kMaxDepth) continue;
-    double mn = iv.lo, mx = iv.hi, mid = 0.0;
-    if (iv.atlo - iv.athi == 1) {
+    --sp;
+    const double ilo = stk.lohi[(2 * sp) * kStkLanes], ihi = stk.lohi[(2 * sp + 1) * kStkLanes];
+    const int iatlo = stk.ints[(4 * sp) * kStkLanes], iathi = stk.ints[(4 * sp + 1) * kStkLanes];
+    const int ioff = stk.ints[(4 * sp + 2) * kStkLanes], idepth = stk.ints[(4 * sp + 3) * kStkLanes];
+    if (idepth >= kMaxDepth) continue;
+    double mn = ilo, mx = ihi, mid = 0.0;
+    if (iatlo - iathi == 1) {
       double v;
       if (falsi_any_r(S, mn, mx, &v)) {
-        if (iv.off >= 0 && iv.off < 10) roots[iv.off] = v;
+        put_root(roots, ioff, v);
         continue;
       }
       for (int it = 0; it < kMaxIt; ++it) {
@@ -749,37 +807,154 @@ __device__ void isolate_r(const SturmR& S, double lo, double hi, int atlo, int a
         if (fabs(mid) > kRelErr) {
           if (fabs((mx - mn) / mid) < kRelErr) break;
         } else if (fabs(mx - mn) < kRelErr) break;
-        if ((iv.atlo - atmid) == 0) mn = mid; else mx = mid;
+        if ((iatlo - atmid) == 0) mn = mid; else mx = mid;
       }
-      if (iv.off >= 0 && iv.off < 10) roots[iv.off] = mid;
+      put_root(roots, ioff, mid);
       continue;
     }
     int it;
     for (it = 0; it < kMaxIt; ++it) {
       mid = (double)((mn + mx) / 2);
       const int atmid = sign_changes_r(S, mid);
-      const int n1 = iv.atlo - atmid, n2 = atmid - iv.athi;
+      const int n1 = iatlo - atmid, n2 = atmid - iathi;
       if (n1 != 0 && n2 != 0) {
-        if (sp + 2 <= 24) {
-          stk[sp++] = Iv{mid, mx, atmid, iv.athi, iv.off + n1, iv.depth + 1};
-          stk[sp++] = Iv{mn, mid, iv.atlo, atmid, iv.off, iv.depth + 1};
+        if (sp + 2 <= kStkDepth) {
+          stk.put(sp++, mid, mx, atmid, iathi, ioff + n1, idepth + 1);
+          stk.put(sp++, mn, mid, iatlo, atmid, ioff, idepth + 1);
         }
         break;
       }
       if (n1 == 0) mn = mid; else mx = mid;
     }
     if (it == kMaxIt)
-      for (int r = iv.athi; r < iv.atlo; ++r) {
-        const int slot = iv.off + r - iv.athi;
-        if (slot >= 0 && slot < 10) roots[slot] = mid;
-      }
+      for (int r = iathi; r < iatlo; ++r) put_root(roots, ioff + r - iathi, mid);
   }
+}
+
+// buildsturm + modp (sturm.cu:285-360) on registers, for the generic case in
+// which every remainder keeps its full degree (ord[k] = 10 - k: no leading
+// coefficient falls under kSmall before the last step).  The operations are
+// remainder_into's, in its order, with every index static, so the sequence
+// never touches scratch (the general form lives in a 1 KB local array whose
+// every access waited on scratch memory: ~95 % of k_roots' time).  Returns
+// false, with R unspecified, when a remainder would be truncated; the caller
+// then takes the general path.
+template <int K>
+__device__ __forceinline__ bool sturm_step_r(SturmR& R) {
+  constexpr int uo = 12 - K, vo = 11 - K;
+  constexpr int ou = sturm_off(K - 2), ov = sturm_off(K - 1), orr = sturm_off(K);
+  double t[uo + 1];
+#pragma unroll
+  for (int i = 0; i <= uo; ++i) t[i] = R.c[ou + i];
+  if (R.c[ov + vo] < 0.0) {
+    t[0] = -t[0];                                 // k = uo - vo - 1 = 0
+#pragma unroll
+    for (int k = 1; k >= 0; --k)
+#pragma unroll
+      for (int j = vo + k - 1; j >= k; --j) t[j] = -t[j] - t[vo + k] * R.c[ov + j - k];
+  } else {
+#pragma unroll
+    for (int k = 1; k >= 0; --k)
+#pragma unroll
+      for (int j = vo + k - 1; j >= k; --j) t[j] -= t[vo + k] * R.c[ov + j - k];
+  }
+  if constexpr (K < 10) {
+    if (fabs(t[vo - 1]) < kSmall) return false;   // would truncate: general path
+    const double g = -fabs(t[vo - 1]);
+#pragma unroll
+    for (int i = vo - 1; i >= 0; --i) R.c[orr + i] = t[i] / g;
+    return sturm_step_r<K + 1>(R);
+  } else {
+    // K = 10: the remainder has order 0 and ends the sequence (np = 10); its
+    // constant is truncated to 0 when small and then negated, as buildsturm does
+    const double c0 = fabs(t[0]) < kSmall ? 0.0 : t[0];
+    R.c[orr] = -c0;
+    return true;
+  }
+}
+
+// Leading coefficients' sign changes at -inf / +inf (numroots, sturm.cu:393-439)
+// for the generic orders ord[i] = 10 - i.
+__device__ __forceinline__ int count_real_roots_r(const SturmR& R, int* atneg, int* atpos) {
+  int pos = 0, neg = 0;
+  double lf = R.c[sturm_off(0) + 10];
+#pragma unroll
+  for (int i = 1; i <= 10; ++i) {
+    const double f = R.c[sturm_off(i) + 10 - i];
+    if (lf == 0.0 || lf * f < 0) ++pos;
+    lf = f;
+  }
+  lf = R.c[sturm_off(0) + 10];                    // ord 0 = 10, even
+#pragma unroll
+  for (int i = 1; i <= 10; ++i) {
+    const double l = R.c[sturm_off(i) + 10 - i];
+    const double f = ((10 - i) & 1) ? -l : l;
+    if (lf == 0.0 || lf * f < 0) ++neg;
+    lf = f;
+  }
+  *atneg = neg;
+  *atpos = pos;
+  return neg - pos;
 }
 
 // find_real_roots_sturm (sturm.cu:557-676) with the iterative part on the
 // register-resident sequence; identical results to real_roots.
-__device__ int real_roots_r(const double poly[11], double roots[10]) {
+__device__ __forceinline__ int real_roots_r(const double poly[11], double roots[10], const IsoStack& stk) {
   SturmR R;
+#ifdef SFM_ROOTS_STATS
+  unsigned long long ts = __builtin_amdgcn_s_memtime();
+#endif
+  // normalisation and root scaling (sturm.cu:570-590) on registers
+  double c0[11];
+  {
+    const double norm = 1.0 / poly[10];
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) c0[i] = poly[i] * norm;
+  }
+  double fac = 1.0;
+  {
+    const double v0 = fabs(c0[0]);
+    if (v0 > 10.0) {
+      fac = cr_pow(v0, -1.0 / 10);
+      double m = fac;
+#pragma unroll
+      for (int i = 9; i >= 0; --i) { c0[i] *= m; m = m * fac; }
+    }
+  }
+  ROOTS_PHASE(0, ts);
+  bool generic;
+  {
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) R.c[sturm_off(0) + i] = c0[i];
+    const double f = fabs(c0[10] * 10);
+#pragma unroll
+    for (int i = 1; i <= 10; ++i) R.c[sturm_off(1) + i - 1] = c0[i] * i / f;
+    generic = sturm_step_r<2>(R);
+  }
+  if (generic) {
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) R.ord[i] = 10 - i;
+    R.np = 10;
+    int atmin, atmax;
+    int nr = count_real_roots_r(R, &atmin, &atmax);
+    ROOTS_PHASE(1, ts);
+    if (nr == 0) return 0;
+    double mn = -1.0;
+    int nch = sign_changes_r(R, mn);
+    for (int i = 0; nch != atmin && i != kMaxPow; ++i) { mn *= 10.0; nch = sign_changes_r(R, mn); }
+    if (nch != atmin) atmin = nch;
+    double mx = 1.0;
+    nch = sign_changes_r(R, mx);
+    for (int i = 0; nch != atmax && i != kMaxPow; ++i) { mx *= 10.0; nch = sign_changes_r(R, mx); }
+    if (nch != atmax) atmax = nch;
+    nr = atmin - atmax;
+    ROOTS_PHASE(2, ts);
+    if (nr <= 0) return nr;
+    isolate_r(R, mn, mx, atmin, atmax, roots, stk);
+    for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
+    ROOTS_PHASE(3, ts);
+    return nr;
+  }
   {
     Sturm S;
     for (int i = 0; i < 11; ++i) { S.ord[i] = 0; for (int j = 0; j < 11; ++j) S.c[i][j] = 0.0; }
@@ -814,7 +989,7 @@ __device__ int real_roots_r(const double poly[11], double roots[10]) {
     if (nch != atmax) atmax = nch;
     nr = atmin - atmax;
     if (nr <= 0) return nr;
-    isolate_r(R, mn, mx, atmin, atmax, roots);
+    isolate_r(R, mn, mx, atmin, atmax, roots, stk);
     for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
     return nr;
   }

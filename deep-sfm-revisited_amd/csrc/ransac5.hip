@@ -212,23 +212,58 @@ __global__ __launch_bounds__(64) void k_solve_front(const Src src, PairParams pp
   for (int i = 0; i <= 10; ++i) st_at(st, stride, kStPoly + i, hb) = poly[i];
 }
 
+#ifdef SFM_ROOTS_STATS
+__device__ unsigned long long g_roots_cycles[1 << 17];
+extern "C" int sfm_experiment_roots_stats(unsigned int* evals, unsigned int* falsi, unsigned long long* cycles,
+                                          unsigned long long* phases, int n, int reset) {
+  if (reset) {
+    static unsigned int z4[1 << 17];
+    static unsigned long long z8[1 << 17];
+    static unsigned long long zp[4][1 << 17];
+    return (hipMemcpyToSymbol(HIP_SYMBOL(g_roots_evals), z4, sizeof(z4)) == hipSuccess &&
+            hipMemcpyToSymbol(HIP_SYMBOL(g_roots_falsi), z4, sizeof(z4)) == hipSuccess &&
+            hipMemcpyToSymbol(HIP_SYMBOL(g_roots_phase), zp, sizeof(zp)) == hipSuccess &&
+            hipMemcpyToSymbol(HIP_SYMBOL(g_roots_cycles), z8, sizeof(z8)) == hipSuccess) ? 0 : 2;
+  }
+  return (hipMemcpyFromSymbol(evals, HIP_SYMBOL(g_roots_evals), n * 4) == hipSuccess &&
+          hipMemcpyFromSymbol(falsi, HIP_SYMBOL(g_roots_falsi), n * 4) == hipSuccess &&
+          hipMemcpyFromSymbol(phases, HIP_SYMBOL(g_roots_phase), 4 * (1 << 17) * 8) == hipSuccess &&
+          hipMemcpyFromSymbol(cycles, HIP_SYMBOL(g_roots_cycles), n * 8) == hipSuccess) ? 0 : 2;
+}
+#endif
+
 __global__ __launch_bounds__(64) void k_roots(int H, int lanes, double* __restrict__ st, size_t stride,
                                               int32_t* __restrict__ out_nroots) {
   const int b = blockIdx.y;
   if ((int)threadIdx.x >= lanes) return;
   const int h = blockIdx.x * lanes + threadIdx.x;
   if (h >= H) return;
+#ifdef SFM_ROOTS_STATS
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
   const size_t hb = (size_t)b * H + h;
   double poly[11];
 #pragma unroll
   for (int i = 0; i <= 10; ++i) poly[i] = st_at(st, stride, kStPoly + i, hb);
+#ifdef SFM_ROOTS_STATS
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long tl = __builtin_amdgcn_s_memtime();
+  g_roots_cycles[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x + (1 << 16)] = tl - t0;
+#endif
   double roots[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) roots[i] = 0.0;
-  const int nr = real_roots_r(poly, roots);
+  __shared__ double s_lohi[kStkDepth * 2 * kStkLanes];
+  __shared__ int s_ints[kStkDepth * 4 * kStkLanes];
+  const IsoStack stk{s_lohi + threadIdx.x, s_ints + threadIdx.x};
+  const int nr = real_roots_r(poly, roots, stk);
 #pragma unroll
   for (int i = 0; i < 10; ++i) st_at(st, stride, kStRoots + i, hb) = roots[i];
   out_nroots[hb] = nr;
+#ifdef SFM_ROOTS_STATS
+  g_roots_cycles[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x] =
+      __builtin_amdgcn_s_memtime() - t0;
+#endif
 }
 
 __global__ __launch_bounds__(64) void k_solve_back(int H, int cheir, const double* __restrict__ st, size_t stride,

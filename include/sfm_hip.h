@@ -284,7 +284,7 @@ int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int chann
  *
  *   launch shape only -- outputs are bit-identical for every value:
  *     "solve_lanes"           1..64   lanes per wave in k_solve_front (32)
- *     "roots_lanes"           1..64   lanes per wave in k_roots (32)
+ *     "roots_lanes"           1..32   lanes per wave in k_roots (32)
  *     "sweep_lane_pixels"     0..2    pixel-to-lane mapping of the per-row sweep (0)
  *     "sweep_items_per_block" 1,2,4,8 work items per block of the per-row sweep (4)
  *     "sweep_nj"              1,2,4   pixels per lane of k_sweep_tile (1; bf16 uses 2)

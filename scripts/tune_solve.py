@@ -21,8 +21,8 @@ def timed(reps=3):
 
 res = {}
 for rnd in range(3):
-    for fl in (16, 32, 64):
-        for rl in (16, 32, 64):
+    for fl in (8, 16, 32, 64):
+        for rl in (4, 8, 16, 32):
             _lib.tune("solve_lanes", fl); _lib.tune("roots_lanes", rl)
             res.setdefault((fl, rl), []).append(timed())
             E, P, inl, _ = hp.pose(flow, K)
