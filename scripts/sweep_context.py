@@ -1,5 +1,5 @@
 """Sweep launch time in the bench context (right after the RANSAC step) vs
-after an idle gap, for the per-row and aligned-slab kernels."""
+after an idle gap, for the per-row, aligned-slab and narrow-window kernels."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "deep-sfm-revisited_amd"))
@@ -22,8 +22,8 @@ def sweep_ms(n):
 
 
 for rnd in range(2):
-    for flat, grp in ((0, 4), (1, 4), (1, 8)):
-        _lib.tune("sweep_flat", flat); _lib.tune("sweep_group", grp)
+    for flat, grp, nj in ((1, 8, 1), (2, 8, 1), (2, 8, 2), (2, 4, 2), (2, 8, 4)):
+        _lib.tune("sweep_flat", flat); _lib.tune("sweep_group", grp); _lib.tune("sweep_nj", nj)
         res = {}
         for mode in ("after_ransac", "gap_5ms", "gap_50ms", "sweep_only"):
             for _ in range(2):
@@ -41,6 +41,6 @@ for rnd in range(2):
                 torch.cuda.synchronize(); _lib.profile_enable(False)
                 per.append(sweep_ms(1))
             res[mode] = per
-        print(f"flat={flat} group={grp}: " + "; ".join(f"{m} {[round(x, 3) for x in v]}" for m, v in res.items()),
+        print(f"flat={flat} group={grp} nj={nj}: " + "; ".join(f"{m} {[round(x, 3) for x in v]}" for m, v in res.items()),
               flush=True)
-_lib.tune("sweep_flat", 1); _lib.tune("sweep_group", 8)
+_lib.tune("sweep_flat", 2); _lib.tune("sweep_group", 8); _lib.tune("sweep_nj", 1)
