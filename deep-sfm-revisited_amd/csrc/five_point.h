@@ -681,87 +681,17 @@ __device__ __forceinline__ int sign_changes_r(const SturmR& S, double a) {
   return ch;
 }
 
-// modrf_pos (sturm.cu:43-207) on the register copy of s[0].  This and the
-// functions below are force-inlined: a SturmR passed by reference to an
-// outlined call has to live in memory (scratch), and every Horner step of
-// the isolation then waited on it (95 % of k_roots' time).
-__device__ __forceinline__ int falsi_r(const SturmR& S, double a, double b, double* val, bool inv) {
-  const double* c = S.c;   // s[0] occupies c[0..10]
-  if (inv) { double t = a; a = 1.0 / b; b = 1.0 / t; }
-  double fa, fb;
-  if (inv) {
-    fa = fb = c[0];
-#pragma unroll
-    for (int i = 1; i <= 10; ++i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
-  } else {
-    fa = fb = c[10];
-#pragma unroll
-    for (int i = 9; i >= 0; --i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
-  }
-  if (fa * fb > 0.0) return 0;
-  if (fabs(fa) < kRelErr) { *val = inv ? 1.0 / a : a; return 1; }
-  if (fabs(fb) < kRelErr) { *val = inv ? 1.0 / b : b; return 1; }
-  double lfx = fa;
-  for (int it = 0; it < kMaxIt; ++it) {
-    ROOTS_COUNT(g_roots_falsi);
-    const double x = (fb * a - fa * b) / (fb - fa);
-    double fx;
-    if (inv) {
-      fx = c[0];
-#pragma unroll
-      for (int i = 1; i <= 10; ++i) fx = x * fx + c[i];
-    } else {
-      fx = c[10];
-#pragma unroll
-      for (int i = 9; i >= 0; --i) fx = x * fx + c[i];
-    }
-    if (fabs(x) > kRelErr && fabs(fx / x) < kRelErr) { *val = inv ? 1.0 / x : x; return 1; }
-    else if (fabs(fx) < kRelErr) { *val = inv ? 1.0 / x : x; return 1; }
-    if ((fa * fx) < 0) { b = x; fb = fx; if ((lfx * fx) > 0) fa /= 2; }
-    else { a = x; fa = fx; if ((lfx * fx) > 0) fb /= 2; }
-    if (fabs(b - a) < fabs(kRelErr * a)) { *val = inv ? 1.0 / a : a; return 1; }
-    lfx = fx;
-  }
-  return 0;
-}
-
-// modrf (sturm.cu:218-275), leading coefficient omitted at +-1 as in the
-// reference; the case analysis picks (a, b, inverted) for one falsi_r call
-__device__ __forceinline__ int falsi_any_r(const SturmR& S, double a, double b, double* val) {
-  const double* c = S.c;
-  if (a > b) { double t = a; a = b; b = t; }
-  bool inv;
-  if (b <= 1.0 && a >= -1.0) {
-    inv = false;
-  } else if (a >= 1.0 || b <= -1.0) {
-    inv = true;
-  } else {
-    double fp1 = 0.0, fm1 = 0.0, fa = 0.0, fb = 0.0;
-#pragma unroll
-    for (int i = 9; i >= 0; --i) {
-      fp1 = c[i] + fp1;
-      fm1 = c[i] - fm1;
-      fa = a * fa + c[i];
-      fb = b * fb + c[i];
-    }
-    if (a < -1.0 && b > 1.0) {
-      if (fa * fm1 < 0.0) { b = -1.0; inv = true; }
-      else if (fb * fp1 < 0.0) { a = 1.0; inv = true; }
-      else { a = -1.0; b = 1.0; inv = false; }
-    } else if (a < -1.0) {
-      if (fa * fm1 < 0.0) { b = -1.0; inv = true; }
-      else { a = -1.0; inv = false; }
-    } else {
-      if (fb * fp1 < 0.0) { a = 1.0; inv = true; }
-      else { b = 1.0; inv = false; }
-    }
-  }
-  return falsi_r(S, a, b, val, inv);
-}
+// The isolation below is force-inlined into its caller: a SturmR passed by
+// reference to an outlined call has to live in memory (scratch), and every
+// Horner step then waited on it (95 % of k_roots' time).
 
 // Work stack of isolate_r in LDS, one column per lane (stride kStkLanes), so
 // that pushes and pops cost an LDS round trip instead of a scratch one.
-constexpr int kStkDepth = 24;
+// Depth-first, a node at depth d is processed with at most one pending sibling
+// per level 1..d on the stack, and only nodes at depth < kMaxDepth split, so
+// the stack never holds more than kMaxDepth + 1 entries and the capacity test
+// below (the reference's 24-entry array) never fails at 12 either.
+constexpr int kStkDepth = kMaxDepth + 2;
 constexpr int kStkLanes = 32;
 struct IsoStack {
   double* lohi;   // [kStkDepth][2][kStkLanes] + lane
@@ -783,51 +713,161 @@ __device__ __forceinline__ void put_root(double roots[10], int off, double v) {
     if (i == off) roots[i] = v;
 }
 
-// sbisect<depth> (sturm.cu:450-555) as an explicit depth-first work stack
+// sbisect<depth> (sturm.cu:450-555) with modrf (218-275) as a per-lane state
+// machine over an explicit depth-first work stack.  Each pass of the loop
+// advances every lane by one unit of work: popping an interval (with modrf's
+// case analysis and end-point evaluations), one regula-falsi step, or one
+// bisection step (one Sturm-sequence evaluation, shared by the single-root and
+// multi-root bisections).  A wave's time then follows its longest lane's step
+// count; nested loops (falsi and bisection inside the stack loop) made every
+// lane wait for the slowest lane's inner loop at each level.  Each lane runs
+// exactly the operations of sbisect/modrf in their order: results are
+// unchanged (the single-root bisection skips the Sturm evaluation of the step
+// that stops it, whose count the reference discards).
 __device__ __forceinline__ void isolate_r(const SturmR& S, double lo, double hi, int atlo, int athi, double roots[10],
                                           const IsoStack& stk) {
+  constexpr int kPop = 0, kFalsi = 1, kBis1 = 2, kBisN = 3;
+  const double* c = S.c;   // s[0] occupies c[0..10]
   int sp = 0;
   stk.put(sp++, lo, hi, atlo, athi, 0, 0);
-  while (sp > 0) {
-    --sp;
-    const double ilo = stk.lohi[(2 * sp) * kStkLanes], ihi = stk.lohi[(2 * sp + 1) * kStkLanes];
-    const int iatlo = stk.ints[(4 * sp) * kStkLanes], iathi = stk.ints[(4 * sp + 1) * kStkLanes];
-    const int ioff = stk.ints[(4 * sp + 2) * kStkLanes], idepth = stk.ints[(4 * sp + 3) * kStkLanes];
-    if (idepth >= kMaxDepth) continue;
-    double mn = ilo, mx = ihi, mid = 0.0;
-    if (iatlo - iathi == 1) {
-      double v;
-      if (falsi_any_r(S, mn, mx, &v)) {
-        put_root(roots, ioff, v);
-        continue;
-      }
-      for (int it = 0; it < kMaxIt; ++it) {
-        mid = (double)((mn + mx) / 2);
-        const int atmid = sign_changes_r(S, mid);
-        if (fabs(mid) > kRelErr) {
-          if (fabs((mx - mn) / mid) < kRelErr) break;
-        } else if (fabs(mx - mn) < kRelErr) break;
-        if ((iatlo - atmid) == 0) mn = mid; else mx = mid;
-      }
-      put_root(roots, ioff, mid);
-      continue;
-    }
-    int it;
-    for (it = 0; it < kMaxIt; ++it) {
-      mid = (double)((mn + mx) / 2);
-      const int atmid = sign_changes_r(S, mid);
-      const int n1 = iatlo - atmid, n2 = atmid - iathi;
-      if (n1 != 0 && n2 != 0) {
-        if (sp + 2 <= kStkDepth) {
-          stk.put(sp++, mid, mx, atmid, iathi, ioff + n1, idepth + 1);
-          stk.put(sp++, mn, mid, iatlo, atmid, ioff, idepth + 1);
+  int mode = kPop, it = 0;
+  int iatlo = 0, iathi = 0, ioff = 0, idepth = 0;
+  double mn = 0.0, mx = 0.0, mid = 0.0;
+  double fa = 0.0, fb = 0.0, a = 0.0, b = 0.0, lfx = 0.0;
+  bool inv = false;
+  for (;;) {
+    if (mode == kPop) {
+      if (sp == 0) break;
+      --sp;
+      mn = stk.lohi[(2 * sp) * kStkLanes];
+      mx = stk.lohi[(2 * sp + 1) * kStkLanes];
+      iatlo = stk.ints[(4 * sp) * kStkLanes];
+      iathi = stk.ints[(4 * sp + 1) * kStkLanes];
+      ioff = stk.ints[(4 * sp + 2) * kStkLanes];
+      idepth = stk.ints[(4 * sp + 3) * kStkLanes];
+      if (idepth >= kMaxDepth) continue;
+      it = 0;
+      if (iatlo - iathi != 1) {
+        mode = kBisN;
+      } else {
+        // modrf (sturm.cu:218-275): pick (a, b, inverted), then modrf_pos's
+        // end-point evaluations (sturm.cu:43-80)
+        a = mn;
+        b = mx;
+        if (a > b) { const double t = a; a = b; b = t; }
+        if (b <= 1.0 && a >= -1.0) {
+          inv = false;
+        } else if (a >= 1.0 || b <= -1.0) {
+          inv = true;
+        } else {
+          double fp1 = 0.0, fm1 = 0.0, ga = 0.0, gb = 0.0;
+#pragma unroll
+          for (int i = 9; i >= 0; --i) {
+            fp1 = c[i] + fp1;
+            fm1 = c[i] - fm1;
+            ga = a * ga + c[i];
+            gb = b * gb + c[i];
+          }
+          if (a < -1.0 && b > 1.0) {
+            if (ga * fm1 < 0.0) { b = -1.0; inv = true; }
+            else if (gb * fp1 < 0.0) { a = 1.0; inv = true; }
+            else { a = -1.0; b = 1.0; inv = false; }
+          } else if (a < -1.0) {
+            if (ga * fm1 < 0.0) { b = -1.0; inv = true; }
+            else { a = -1.0; inv = false; }
+          } else {
+            if (gb * fp1 < 0.0) { a = 1.0; inv = true; }
+            else { b = 1.0; inv = false; }
+          }
         }
-        break;
+        if (inv) { const double t = a; a = 1.0 / b; b = 1.0 / t; }
+        if (inv) {
+          fa = fb = c[0];
+#pragma unroll
+          for (int i = 1; i <= 10; ++i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
+        } else {
+          fa = fb = c[10];
+#pragma unroll
+          for (int i = 9; i >= 0; --i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
+        }
+        if (fa * fb > 0.0) {
+          mode = kBis1;                              // modrf failed: bisection on [mn, mx]
+        } else if (fabs(fa) < kRelErr) {
+          put_root(roots, ioff, inv ? 1.0 / a : a);  // stays kPop
+        } else if (fabs(fb) < kRelErr) {
+          put_root(roots, ioff, inv ? 1.0 / b : b);
+        } else {
+          lfx = fa;
+          mode = kFalsi;
+        }
       }
-      if (n1 == 0) mn = mid; else mx = mid;
     }
-    if (it == kMaxIt)
-      for (int r = iathi; r < iatlo; ++r) put_root(roots, ioff + r - iathi, mid);
+    if (mode == kFalsi) {
+      // one iteration of modrf_pos's loop (sturm.cu:82-205)
+      ROOTS_COUNT(g_roots_falsi);
+      const double x = (fb * a - fa * b) / (fb - fa);
+      double fx;
+      if (inv) {
+        fx = c[0];
+#pragma unroll
+        for (int i = 1; i <= 10; ++i) fx = x * fx + c[i];
+      } else {
+        fx = c[10];
+#pragma unroll
+        for (int i = 9; i >= 0; --i) fx = x * fx + c[i];
+      }
+      bool found = false;
+      double v = x;
+      if (fabs(x) > kRelErr && fabs(fx / x) < kRelErr) found = true;
+      else if (fabs(fx) < kRelErr) found = true;
+      if (!found) {
+        if ((fa * fx) < 0) { b = x; fb = fx; if ((lfx * fx) > 0) fa /= 2; }
+        else { a = x; fa = fx; if ((lfx * fx) > 0) fb /= 2; }
+        if (fabs(b - a) < fabs(kRelErr * a)) {
+          found = true;
+          v = a;
+        } else {
+          lfx = fx;
+          if (++it == kMaxIt) { mode = kBis1; it = 0; }   // modrf_pos gave up
+        }
+      }
+      if (found) { put_root(roots, ioff, inv ? 1.0 / v : v); mode = kPop; }
+    } else if (mode >= kBis1) {
+      mid = (double)((mn + mx) / 2);
+      bool stop = false;
+      if (mode == kBis1) {
+        if (fabs(mid) > kRelErr) stop = fabs((mx - mn) / mid) < kRelErr;
+        else stop = fabs(mx - mn) < kRelErr;
+      }
+      if (!stop) {
+        const int atmid = sign_changes_r(S, mid);
+        if (mode == kBis1) {
+          if ((iatlo - atmid) == 0) mn = mid; else mx = mid;
+          stop = ++it == kMaxIt;
+        } else {
+          const int n1 = iatlo - atmid, n2 = atmid - iathi;
+          if (n1 != 0 && n2 != 0) {
+            if (sp + 2 <= kStkDepth) {
+              stk.put(sp++, mid, mx, atmid, iathi, ioff + n1, idepth + 1);
+              stk.put(sp++, mn, mid, iatlo, atmid, ioff, idepth + 1);
+            }
+            mode = kPop;
+          } else {
+            // An interval that no longer changes (it has shrunk to adjacent
+            // doubles around a multiple root) repeats this step until the
+            // iteration limit, with the same mid: jump to the limit.
+            const bool fixed = (n1 == 0) ? mid == mn : mid == mx;
+            if (n1 == 0) mn = mid; else mx = mid;
+            if (fixed) it = kMaxIt - 1;
+            if (++it == kMaxIt) {
+              for (int r = iathi; r < iatlo; ++r) put_root(roots, ioff + r - iathi, mid);
+              mode = kPop;
+            }
+          }
+        }
+      }
+      if (stop) { put_root(roots, ioff, mid); mode = kPop; }
+    }
   }
 }
 

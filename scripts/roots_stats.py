@@ -12,7 +12,9 @@ from sfm_amd.pipeline import TwoViewHotPath
 dev = torch.device("cuda", 0)
 B = 8
 flow, K, _, _ = synth.kitti_pair_batch(B, seed=1000, device=dev)
-hp = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 128, 8, 1e-4, 1.0, True, 0.6, device=dev)
+# --sparse: the SIFT-keypoint branch (bench.py --config sparse, 2,048 keypoints per pair)
+kp = (synth.keypoints(B, 2048, (376, 1242), seed=0, device=dev), [2048] * B) if "--sparse" in sys.argv else None
+hp = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 128, 8, 1e-4, 1.0, True, 0.6, device=dev, keypoints=kp)
 hp.pose(flow, K); torch.cuda.synchronize()
 lib = _lib.load()
 n = 1 << 17

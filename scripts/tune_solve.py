@@ -8,7 +8,9 @@ from sfm_amd.pipeline import TwoViewHotPath
 dev = torch.device("cuda", 0)
 B = 8
 flow, K, pose, _ = synth.kitti_pair_batch(B, seed=1000, device=dev)
-hp = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 128, 8, 1e-4, 1.0, True, 0.6, device=dev)
+# --sparse: the SIFT-keypoint branch (bench.py --config sparse, 2,048 keypoints per pair)
+kp = (synth.keypoints(B, 2048, (376, 1242), seed=0, device=dev), [2048] * B) if "--sparse" in sys.argv else None
+hp = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 128, 8, 1e-4, 1.0, True, 0.6, device=dev, keypoints=kp)
 E0, P0, inl0, _ = hp.pose(flow, K)
 E0 = E0.clone(); inl0 = inl0.clone()
 
