@@ -90,9 +90,10 @@ struct TuneKey {
   bool (*ok)(int);
 };
 bool v_1_64(int v) { return v >= 1 && v <= 64; }
+bool v_1_16(int v) { return v >= 1 && v <= 16; }
 bool v_01(int v) { return v == 0 || v == 1; }
 const TuneKey kTuneKeys[] = {
-    {"solve_lanes", &sfm::Tuning::solve_lanes, v_1_64},
+    {"solve_lanes", &sfm::Tuning::solve_lanes, v_1_16},
     {"roots_lanes", &sfm::Tuning::roots_lanes, [](int v) { return v >= 1 && v <= 32; }},   // LDS stack columns
     {"sweep_lane_pixels", &sfm::Tuning::sweep_lane_pixels, [](int v) { return v >= 0 && v <= 2; }},
     {"sweep_items_per_block", &sfm::Tuning::sweep_items_per_block,

@@ -151,7 +151,7 @@ __device__ __forceinline__ void essential_basis(const double q[5][2], const doub
 }
 
 // Constraint equations (EEeqns_5pt, essential_matrix_5pt.cu:428-474)
-__device__ void build_equations(const Lin Eb[9], Eqs& A) {
+__device__ __forceinline__ void build_equations(const Lin Eb[9], Eqs& A) {
   // trace(E E^T), row-major element order (traceEEt)
   Quad tr = qmul(Eb[0], Eb[0]);
 #pragma unroll
@@ -245,7 +245,7 @@ __device__ __forceinline__ void pivot_rows(Eqs& A, int last) {
 }
 
 // reduce_Ematrix (essential_matrix_5pt.cu:852-900)
-__device__ void reduce_equations(Eqs& A) {
+__device__ __forceinline__ void reduce_equations(Eqs& A) {
   for (int c = 9; c >= 3; --c) {
     pivot_rows(A, c);
     const double pv = A.e0[c][c];
@@ -296,7 +296,7 @@ __device__ __forceinline__ double coef(const Eqs& A, int deg, int r, int c) {
 }
 
 // Degree-10 determinant polynomial (compute_determinant / one_cofactor, 902-948)
-__device__ void determinant_poly(const Eqs& A, double poly[11]) {
+__device__ __forceinline__ void determinant_poly(const Eqs& A, double poly[11]) {
 #pragma unroll
   for (int i = 0; i <= 10; ++i) poly[i] = 0.0;
   const int rr[3][3] = {{0, 1, 2}, {1, 2, 0}, {2, 0, 1}};

@@ -162,6 +162,7 @@ struct FlowSrc {
 // The state in between (116 doubles per hypothesis) is stored field-major.
 __device__ __forceinline__ double& st_at(double* st, size_t stride, int f, size_t hb) { return st[f * stride + hb]; }
 
+constexpr int kFrontLanes = 16;   // upper bound of the solve_lanes key
 template <class Src>
 __global__ __launch_bounds__(64) void k_solve_front(const Src src, PairParams pp, int H, uint64_t seed, int lanes,
                                                     double* __restrict__ st, size_t stride) {
@@ -180,7 +181,12 @@ __global__ __launch_bounds__(64) void k_solve_front(const Src src, PairParams pp
   }
   Lin Eb[9];
   essential_basis(q, qp, Eb);
-  Eqs A;
+  // The equation set (1784 B) lives in LDS, one record per lane: the
+  // reduction's pivoting indexes rows dynamically, which put it in scratch
+  // (0.30 -> 0.13 ms per 32,768 hypotheses).  A 1784-B lane stride is 446
+  // dwords, so the 16 lanes' doubles fall in distinct bank pairs.
+  __shared__ Eqs s_eqs[kFrontLanes];
+  Eqs& A = s_eqs[threadIdx.x];
   build_equations(Eb, A);
   reduce_equations(A);
   double poly[11];
@@ -1600,12 +1606,14 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   }
   {
     ProfScope ps("ransac_solve", s);
-    const int lanes = tuning().solve_lanes;
+    // lane counts bounded by the kernels' per-lane LDS records (the key validators enforce it too)
+    const int lanes = std::min(tuning().solve_lanes, kFrontLanes);
+    const int rlanes = std::min(tuning().roots_lanes, kStkLanes);
     const size_t stride = (size_t)bc * H;
     hipLaunchKernelGGL(k_solve_front<Src>, dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H, seed,
                        lanes, w.sstate, stride);
-    hipLaunchKernelGGL(k_roots, dim3((H + tuning().roots_lanes - 1) / tuning().roots_lanes, bc), dim3(64), 0, s, H,
-                       tuning().roots_lanes, w.sstate, stride, w.nroots);
+    hipLaunchKernelGGL(k_roots, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate, stride,
+                       w.nroots);
     hipLaunchKernelGGL(k_solve_back, dim3((H + 63) / 64, bc), dim3(64), 0, s, H, cheir, w.sstate, stride, w.nroots,
                        w.ncand, w.hypE, w.hypP);
   }

@@ -283,7 +283,7 @@ int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int chann
 /* Tuning knobs (process-wide; every key, its accepted values and default):
  *
  *   launch shape only -- outputs are bit-identical for every value:
- *     "solve_lanes"           1..64   lanes per wave in k_solve_front (32)
+ *     "solve_lanes"           1..16   lanes per wave in k_solve_front (16)
  *     "roots_lanes"           1..32   lanes per wave in k_roots (32)
  *     "sweep_lane_pixels"     0..2    pixel-to-lane mapping of the per-row sweep (0)
  *     "sweep_items_per_block" 1,2,4,8 work items per block of the per-row sweep (4)

@@ -23,7 +23,7 @@ def timed(reps=3):
 
 res = {}
 for rnd in range(3):
-    for fl in (8, 16, 32, 64):
+    for fl in (4, 8, 12, 16):
         for rl in (4, 8, 16, 32):
             _lib.tune("solve_lanes", fl); _lib.tune("roots_lanes", rl)
             res.setdefault((fl, rl), []).append(timed())
