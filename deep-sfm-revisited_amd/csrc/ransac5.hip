@@ -411,27 +411,21 @@ __device__ __forceinline__ void fp32_constants(const double* E, double thr, bool
 }
 
 // ---------------------------------------------------------------------------
-// Phase 2: chains and the dense candidate list (one block of 512 per pair)
+// Phase 2: chains and the dense candidate list
+//   k_chain  one block of 512 per pair: exclusive scan of the candidate counts
+//            over chains (chain t owns hypotheses t*iters .. t*iters+iters-1)
+//   k_cand   one thread per (hypothesis, slot): the candidate records
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
-                                                   const int32_t* __restrict__ nroots,
-                                                   const int32_t* __restrict__ ncand,
-                                                   const double* __restrict__ hypE,
-                                                   const double* __restrict__ hypP,
-                                                   double* __restrict__ hypP0,
-                                                   int32_t* __restrict__ cand_off,
-                                                   int32_t* __restrict__ cand_total,
-                                                   double* __restrict__ candE, int cmax, double guard_g,
-                                                   double thr, int fast32) {
+__global__ __launch_bounds__(kChains) void k_chain(int H, int iters, const int32_t* __restrict__ ncand,
+                                                   int32_t* __restrict__ cand_off, int32_t* __restrict__ cand_total) {
   __shared__ int32_t s_sum[kChains / 64];
   const int b = blockIdx.x, t = threadIdx.x;
-  const size_t hb0 = (size_t)b * H;
+  const size_t hb0 = (size_t)b * H + (size_t)t * iters;
   int cnt = 0;
   for (int i = 0; i < iters; ++i) {
-    const int nc = ncand[hb0 + t * iters + i];
+    const int nc = ncand[hb0 + i];
     cnt += nc > 0 ? nc : 1;
   }
-  // block exclusive scan over chains
   const int lane = t & 63, wv = t >> 6;
   int incl = cnt;
 #pragma unroll
@@ -441,53 +435,54 @@ __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, int cheir,
   }
   if (lane == 63) s_sum[wv] = incl;
   __syncthreads();
-  int base = incl - cnt;
-  for (int w = 0; w < wv; ++w) base += s_sum[w];
-  if (t == kChains - 1) cand_total[b] = base + cnt;
-
-  double E0[9], P0[12];
-#pragma unroll
-  for (int e = 0; e < 9; ++e) E0[e] = 0.0;
-#pragma unroll
-  for (int e = 0; e < 12; ++e) P0[e] = 0.0;
-  int off = base;
-  double* cE = candE + (size_t)b * cmax * kCandStride;
+  int off = incl - cnt;
+  for (int w = 0; w < wv; ++w) off += s_sum[w];
+  if (t == kChains - 1) cand_total[b] = off + cnt;
   for (int i = 0; i < iters; ++i) {
-    const int h = t * iters + i;
-    const size_t hb = hb0 + h;
-    const int nr = nroots[hb], nc = ncand[hb];
-    const double* Eh = hypE + hb * kMaxSlots * 9;
-    cand_off[hb] = off;
-    if (nc > 0) {
-      for (int j = 0; j < nc; ++j) {
-        double* dst = cE + (size_t)(off + j) * kCandStride;
-#pragma unroll
-        for (int e = 0; e < 9; ++e) dst[e] = Eh[j * 9 + e];
-        dst[9] = guard_constant(dst, guard_g);
-        fp32_constants(dst, thr, fast32 != 0, reinterpret_cast<float*>(dst + 10));
-      }
-      off += nc;
-    } else {
-      // rescore-only candidate: slot 0 as the reference thread would hold it
-      double* dst = cE + (size_t)off * kCandStride;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) dst[e] = nr > 0 ? Eh[e] : E0[e];
-      dst[9] = guard_constant(dst, guard_g);
-      fp32_constants(dst, thr, fast32 != 0, reinterpret_cast<float*>(dst + 10));
-#pragma unroll
-      for (int e = 0; e < 12; ++e) hypP0[hb * 12 + e] = P0[e];
-      off += 1;
-    }
-    if (nr > 0) {
-#pragma unroll
-      for (int e = 0; e < 9; ++e) E0[e] = Eh[e];
-    }
-    if (cheir && nc > 0) {
-      const double* Ph = hypP + hb * kMaxSlots * 12;
-#pragma unroll
-      for (int e = 0; e < 12; ++e) P0[e] = Ph[e];
-    }
+    const int nc = ncand[hb0 + i];
+    cand_off[hb0 + i] = off;
+    off += nc > 0 ? nc : 1;
   }
+}
+
+// A hypothesis with no candidate rescores slot 0 as the reference thread
+// holds it (kernel_functions.cu:154, 179-214): E of the chain's latest
+// hypothesis with a root, P of its latest with an accepted candidate (zeros
+// before any).  The thread finds them by looking back along its chain.
+__global__ __launch_bounds__(256) void k_cand(int H, int iters, int cheir, const int32_t* __restrict__ nroots,
+                                              const int32_t* __restrict__ ncand, const double* __restrict__ hypE,
+                                              const double* __restrict__ hypP, double* __restrict__ hypP0,
+                                              const int32_t* __restrict__ cand_off, double* __restrict__ candE,
+                                              int cmax, double guard_g, double thr, int fast32) {
+  const int b = blockIdx.y;
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  const int h = g / kMaxSlots, j = g - h * kMaxSlots;
+  if (h >= H) return;
+  const size_t hb0 = (size_t)b * H;
+  const size_t hb = hb0 + h;
+  const int nc = ncand[hb];
+  if (j >= (nc > 0 ? nc : 1)) return;
+  double* dst = candE + ((size_t)b * cmax + cand_off[hb] + j) * kCandStride;
+  if (nc > 0) {
+    const double* Eh = hypE + (hb * kMaxSlots + j) * 9;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) dst[e] = Eh[e];
+  } else {
+    const int i = h % iters;
+    const size_t c0 = hb - i;   // the chain's first hypothesis
+    int ke = -1, kp = -1;
+    for (int k = i; k >= 0 && ke < 0; --k)
+      if (nroots[c0 + k] > 0) ke = k;
+    if (cheir)
+      for (int k = i - 1; k >= 0 && kp < 0; --k)
+        if (ncand[c0 + k] > 0) kp = k;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) dst[e] = ke >= 0 ? hypE[(c0 + ke) * kMaxSlots * 9 + e] : 0.0;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) hypP0[hb * 12 + e] = kp >= 0 ? hypP[(c0 + kp) * kMaxSlots * 12 + e] : 0.0;
+  }
+  dst[9] = guard_constant(dst, guard_g);
+  fp32_constants(dst, thr, fast32 != 0, reinterpret_cast<float*>(dst + 10));
 }
 
 // ---------------------------------------------------------------------------
@@ -1625,8 +1620,9 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   const bool fast32 = fast && thr >= 0x1p-20 && tuning().score_fp32;
   {
     ProfScope ps("ransac_chain", s);
-    hipLaunchKernelGGL(k_chain, dim3(bc), dim3(kChains), 0, s, H, iters, cheir, w.nroots, w.ncand, w.hypE,
-                       w.hypP, w.hypP0, w.cand_off, w.cand_total, w.candE, cmax, guard_g, thr, fast32 ? 1 : 0);
+    hipLaunchKernelGGL(k_chain, dim3(bc), dim3(kChains), 0, s, H, iters, w.ncand, w.cand_off, w.cand_total);
+    hipLaunchKernelGGL(k_cand, dim3((H * kMaxSlots + 255) / 256, bc), dim3(256), 0, s, H, iters, cheir, w.nroots,
+                       w.ncand, w.hypE, w.hypP, w.hypP0, w.cand_off, w.candE, cmax, guard_g, thr, fast32 ? 1 : 0);
   }
   SFM_LAUNCHED();
   SFM_HIP(hipMemsetAsync(w.cntT, 0, (size_t)bc * cmax * 4, s));
