@@ -622,18 +622,30 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
       const int qtotal = __builtin_amdgcn_readlane(incl, 63);
       for (int base = 0; base < qtotal; base += kMfQueue) {
         int pos = incl - nl - base;
-        uint32_t ub[16];
+        if (qtotal <= kMfQueue) {
+          // the usual case, one window: every entry fits, no bounds test.
+          // Entry = row << 24 | point; bit j of a string is tile ntiles-1-j,
+          // point p0 + 32 (ntiles-1-j) + rl = top - 32 j.
+          uint32_t* q = queue + pos;
 #pragma unroll
-        for (int g = 0; g < 16; ++g) ub[g] = ~(s1[g] | s2[g]) & vm;
+          for (int g = 0; g < 16; ++g) {
+            uint32_t u = ~(s1[g] | s2[g]) & vm;
+            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(p0 + 32 * (ntiles - 1) + rl);
+            while (u) {
+              *q++ = top - 32u * (uint32_t)__builtin_ctz(u);
+              u &= u - 1u;
+            }
+          }
+        } else {
 #pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          uint32_t u = ub[g];
-          const uint32_t rowbits = (uint32_t)mf_row(g, hl) << 24;
-          while (u) {
-            const int j = 31 - __clz(u);
-            u &= ~(1u << j);
-            if (pos >= 0 && pos < kMfQueue) queue[pos] = rowbits | (uint32_t)(p0 + 32 * (ntiles - 1 - j) + rl);
-            ++pos;
+          for (int g = 0; g < 16; ++g) {
+            uint32_t u = ~(s1[g] | s2[g]) & vm;
+            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(p0 + 32 * (ntiles - 1) + rl);
+            while (u) {
+              if (pos >= 0 && pos < kMfQueue) queue[pos] = top - 32u * (uint32_t)__builtin_ctz(u);
+              u &= u - 1u;
+              ++pos;
+            }
           }
         }
         wave_sync();

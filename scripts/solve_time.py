@@ -1,8 +1,9 @@
-"""Solve-phase time (k_solve_front + k_roots + k_solve_back, HIP events) of
-the loaded library (SFM_HIP_LIB selects an experiment build) on the bench
-RANSAC, dense or --sparse; outputs are checked against a reference file
-written by the first run (--ref PATH).  Usage:
-  solve_time.py [--sparse] [--ref PATH] [key=value ...]"""
+"""Per-launch time of one RANSAC phase (HIP events; --phase NAME, default
+ransac_solve = k_solve_front + k_roots + k_solve_back; ransac_score = the
+scoring kernels) of the loaded library (SFM_HIP_LIB selects an experiment
+build) on the bench RANSAC, dense or --sparse; outputs are checked against a
+reference file written by the first run (--ref PATH).  Usage:
+  solve_time.py [--sparse] [--ref PATH] [--phase NAME] [key=value ...]"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "deep-sfm-revisited_amd"))
@@ -13,8 +14,8 @@ dev = torch.device("cuda", 0)
 B = 8
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 ref = sys.argv[sys.argv.index("--ref") + 1] if "--ref" in sys.argv else None
-if ref in args:
-    args.remove(ref)
+phase = sys.argv[sys.argv.index("--phase") + 1] if "--phase" in sys.argv else "ransac_solve"
+args = [a for a in args if a not in (ref, phase)]
 for kv in args:
     k, v = kv.split("=")
     _lib.tune(k, int(v))
@@ -34,8 +35,8 @@ for _ in range(5):
     for _ in range(3):
         hp.pose(flow, K)
     torch.cuda.synchronize(); _lib.profile_enable(False)
-    ms, n = _lib.profile_read("ransac_solve")
+    ms, n = _lib.profile_read(phase)
     res.append(ms / max(n, 1))
 res.sort()
 print(f"{os.environ.get('SFM_HIP_LIB', 'default')} {' '.join(args)} {'sparse' if kp else 'dense'}: "
-      f"solve median {res[2]:.4f} ms  min {res[0]:.4f}")
+      f"{phase} median {res[2]:.4f} ms  min {res[0]:.4f}")
