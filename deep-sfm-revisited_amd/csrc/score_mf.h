@@ -53,6 +53,10 @@
 typedef _Float16 mf_half8 __attribute__((ext_vector_type(8)));
 typedef float mf_float16 __attribute__((ext_vector_type(16)));
 
+#ifndef SFM_MF_SUB
+#define SFM_MF_SUB 3
+#endif
+constexpr int kMfSub = SFM_MF_SUB;            // candidate groups per item (one staged span serves them all)
 constexpr int kMfWaves = 12;                // waves per block (3 per SIMD): one 32-candidate tile each
 constexpr int kMfSpan = 768;                // points per item (B fragments staged in LDS)
 constexpr int kMfTiles = kMfSpan / 32;
@@ -459,7 +463,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
     int acc = 0;
     for (int b = 0; b < batch; ++b) {
       const int tiles = (cand_total[b] + kKC - 1) / kKC;
-      const int groups = (tiles + kMfWaves - 1) / kMfWaves;
+      const int groups = (tiles + kMfWaves * kMfSub - 1) / (kMfWaves * kMfSub);
       const int spans = (max(pp.test[b], pp.rtest[b]) + kMfSpan - 1) / kMfSpan;
       s_spans[b] = spans;
       s_first[b] = acc;
@@ -477,7 +481,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
   // item -> (pair, candidate group, span) and its prefetch: the next item's
   // points, A rows and E rows are loaded into registers while the current
   // item computes, so staging costs no global latency
-  struct Item { int b, p0, p1, c0, nc, T, R; };
+  struct Item { int b, p0, p1, c0, nc, T, R; };   // c0, nc: the item's first candidate group
   auto item_of = [&](int item, int b) {                       // b: a pair at or before the item's
     Item it;
     while (item >= s_first[b + 1]) ++b;
@@ -489,7 +493,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
     it.R = pp.rtest[b];
     it.p0 = span * kMfSpan;
     it.p1 = min(max(it.T, it.R), it.p0 + kMfSpan);
-    it.c0 = (group * kMfWaves + wv) * kKC;
+    it.c0 = (group * kMfSub * kMfWaves + wv) * kKC;
     it.nc = max(0, min(kKC, s_ctot[b] - it.c0));
     // wave-uniform by construction; say so, so that addresses stay scalar
     it.b = __builtin_amdgcn_readfirstlane(it.b);
@@ -506,22 +510,14 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
   double4 pv[kPtsPerThread];
   double ev[kEPerLane];
   mf_half8 nA1, nA2, nAL, nAH;
-  auto prefetch = [&](const Item& it) {
-    // an opaque copy of the lane index: the per-lane offsets below are then
-    // recomputed per call instead of being hoisted out of the item loop,
-    // where they would occupy (and spill) registers through the tile loop
+  // one candidate group's E rows (-> s_E at its start) and split-f16 A rows
+  auto prefetch_cands = [&](int b, int c0, int nc) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int lh = ln >> 5, lr = ln & 31;
-#pragma unroll
-    for (int j = 0; j < kPtsPerThread; ++j) {
-      const int i = wv * 64 + ln + j * kMfWaves * 64;
-      const int p = it.p0 + i;
-      pv[j] = src.load(it.b, (i < kMfSpan && p < it.p1) ? p : it.p0);
-    }
-    if (it.nc > 0) {                                         // uniform; record c0 exists
-      const char* rec0 = reinterpret_cast<const char*>(candE + ((size_t)it.b * cmax + it.c0) * kCandStride);
-      const int lim = it.nc * 10;
+    const int lh = ln >> 5, lr = ln & 31;   // lane half and row of the A fragment
+    if (nc > 0) {                                            // uniform; record c0 exists
+      const char* rec0 = reinterpret_cast<const char*>(candE + ((size_t)b * cmax + c0) * kCandStride);
+      const int lim = nc * 10;
 #pragma unroll
       for (int j = 0; j < kEPerLane; ++j) {                  // E (9) + Kg of record i / 10
         const int i = ln + 64 * j;
@@ -529,8 +525,8 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
         ev[j] = *reinterpret_cast<const double*>(rec0 + o);
       }
     }
-    if (lr < it.nc) {
-      const mf_half8* rec = reinterpret_cast<const mf_half8*>(candF + ((size_t)it.b * cmax + it.c0 + lr) * kMfRec);
+    if (lr < nc) {
+      const mf_half8* rec = reinterpret_cast<const mf_half8*>(candF + ((size_t)b * cmax + c0 + lr) * kMfRec);
       nA1 = rec[0 + lh];
       nA2 = rec[2 + lh];
       nAL = rec[4 + lh];
@@ -548,6 +544,20 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
       }
     }
   };
+  auto prefetch = [&](const Item& it) {
+    // an opaque copy of the lane index: the per-lane offsets below are then
+    // recomputed per call instead of being hoisted out of the item loop,
+    // where they would occupy (and spill) registers through the tile loop
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int j = 0; j < kPtsPerThread; ++j) {
+      const int i = wv * 64 + ln + j * kMfWaves * 64;
+      const int p = it.p0 + i;
+      pv[j] = src.load(it.b, (i < kMfSpan && p < it.p1) ? p : it.p0);
+    }
+    prefetch_cands(it.b, it.c0, it.nc);
+  };
   Item cur;
   if (blockIdx.x < total) {
     cur = item_of(blockIdx.x, 0);
@@ -561,7 +571,8 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
 #ifdef SFM_MF_STAMPS
     mf_acc_[7] += 1;
 #endif
-    const int b = cur.b, p0 = cur.p0, p1 = cur.p1, c0 = cur.c0, nc = cur.nc, T = cur.T, R = cur.R;
+    const int b = cur.b, p0 = cur.p0, p1 = cur.p1, T = cur.T, R = cur.R;
+    const int cg0 = cur.c0;
     // 1. stage the prefetched span (points + B columns) and E rows into LDS
 #pragma unroll
     for (int j = 0; j < kPtsPerThread; ++j) {
@@ -576,7 +587,6 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
       const int i = lane + 64 * j;
       if (i < kKC * 10) s_E[wv][i] = ev[j];
     }
-    const mf_half8 A1 = nA1, A2 = nA2, AL = nAL, AH = nAH;
     lds_barrier();
     // 2. the next item's loads fly while this one drains and reduces (issued
     // after the tile loop: its registers are not live during the MFMAs)
@@ -588,7 +598,27 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
       }
     };
     MF_STAMP(0);
-    if (nc <= 0) prefetch_next();
+    // kMfSub candidate groups run over the staged span in turn; each group's
+    // rows were loaded while the previous group drained (unrolled: the last
+    // group's next-item prefetch must not be live through the others)
+#pragma unroll
+    for (int sub = 0; sub < kMfSub; ++sub) {
+    const int c0 = __builtin_amdgcn_readfirstlane(cg0 + sub * kMfWaves * kKC);
+    const int nc = max(0, min(kKC, s_ctot[b] - c0));
+    if (sub > 0) {
+#pragma unroll
+      for (int j = 0; j < kEPerLane; ++j) {
+        const int i = lane + 64 * j;
+        if (i < kKC * 10) s_E[wv][i] = ev[j];
+      }
+      wave_sync();
+    }
+    const mf_half8 A1 = nA1, A2 = nA2, AL = nAL, AH = nAH;
+    auto prefetch_after = [&]() {
+      if (sub + 1 < kMfSub) prefetch_cands(b, c0 + kMfWaves * kKC, max(0, min(kKC, s_ctot[b] - c0 - kMfWaves * kKC)));
+      else prefetch_next();
+    };
+    if (nc <= 0) prefetch_after();
     if (nc > 0) {
       const int ntiles = (p1 - p0 + 31) >> 5;
       uint32_t s1[16], s2[16];
@@ -608,7 +638,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
         mf_tile_decide(r, s1, s2);
       }
       MF_STAMP(1);
-      prefetch_next();
+      prefetch_after();
       MF_STAMP(6);
       // bit n-1-t <-> tile t; dead slots are decided outliers
       const uint32_t vm = ntiles >= 32 ? ~0u : ((1u << ntiles) - 1u);
@@ -688,6 +718,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(k
       }
       wave_sync();
       MF_STAMP(4);
+    }
     }
     lds_barrier();                                            // the span is re-staged next item
     MF_STAMP(5);
