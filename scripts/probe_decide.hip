@@ -10,6 +10,7 @@
 //   6 both, split order: inlier tests (a, Ylo), next tile's Ylo MFMA, outlier
 //     tests (a, Yhi), next tile's a and Yhi MFMAs; sched_barrier between phases
 //   7 both, two accumulator sets (next tile's MFMAs beside this tile's decisions)
+//   8 64 v_fma_f32 only   9 64 v_alignbit_b32 only   10 64 v_lshl_add_u32 only
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fno-slp-vectorize -o probe_decide probe_decide.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -84,6 +85,29 @@ void k_tile(const _Float16* __restrict__ in, unsigned* __restrict__ out, unsigne
       a = a2; l = l2; h = h2;
       continue;
     }
+    if (MODE >= 8) {
+      a[it & 15] += 1.0f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        if (MODE == 8) {
+          l[g] = __builtin_fmaf(a[g], a[g], -l[g]);
+          h[g] = __builtin_fmaf(-a[g], a[g], h[g]);
+          l[g] = __builtin_fmaf(a[g], l[g], -h[g]);
+          h[g] = __builtin_fmaf(-a[g], h[g], l[g]);
+        } else if (MODE == 9) {
+          s1[g] = __builtin_amdgcn_alignbit(s1[g], __float_as_uint(a[g]), 31);
+          s2[g] = __builtin_amdgcn_alignbit(s2[g], __float_as_uint(a[g]), 30);
+          s1[g] = __builtin_amdgcn_alignbit(s1[g], s2[g], 29);
+          s2[g] = __builtin_amdgcn_alignbit(s2[g], s1[g], 28);
+        } else {
+          s1[g] = (s1[g] << 1) + __float_as_uint(a[g]);
+          s2[g] = (s2[g] << 2) + s1[g];
+          s1[g] = (s1[g] << 3) + s2[g];
+          s2[g] = (s2[g] << 1) + s1[g];
+        }
+      }
+      continue;
+    }
     if (MODE == 0 || MODE == 2 || MODE == 3) {
       a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B, zero, 0, 0, 0);
       a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A2, B, a, 0, 0, 0);
@@ -129,7 +153,7 @@ void k_tile(const _Float16* __restrict__ in, unsigned* __restrict__ out, unsigne
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   unsigned r = 0;
 #pragma unroll
-  for (int g = 0; g < 16; ++g) r += s1[g] ^ s2[g];
+  for (int g = 0; g < 16; ++g) r += s1[g] ^ s2[g] ^ __float_as_uint(l[g] + h[g]);
   out[blockIdx.x * blockDim.x + threadIdx.x] = r;
   if (lane == 0) cyc[blockIdx.x * kWaves + (threadIdx.x >> 6)] = t1 - t0;
 }
@@ -146,16 +170,17 @@ int main() {
   hipMemset(in, 0, 4096 * 2);
   hipMalloc(&out, (size_t)cus * kWaves * 64 * 4);
   hipMalloc(&cyc, (size_t)cus * kWaves * 8);
-  void (*ks[8])(const _Float16*, unsigned*, unsigned long long*, int) = {
-      k_tile<0>, k_tile<1>, k_tile<2>, k_tile<3>, k_tile<4>, k_tile<5>, k_tile<6>, k_tile<7>};
-  const char* names[8] = {"MFMA only", "decisions only", "MFMA + decisions", "MFMA + decisions, pk_fma",
+  void (*ks[11])(const _Float16*, unsigned*, unsigned long long*, int) = {
+      k_tile<0>, k_tile<1>, k_tile<2>, k_tile<3>, k_tile<4>, k_tile<5>, k_tile<6>, k_tile<7>,
+      k_tile<8>, k_tile<9>, k_tile<10>};
+  const char* names[11] = {"MFMA only", "decisions only", "MFMA + decisions", "MFMA + decisions, pk_fma",
                           "decisions only, pk_fma", "decisions only, shift+or", "split order",
-                          "two accumulator sets"};
+                          "two accumulator sets", "64 v_fma_f32", "64 v_alignbit_b32", "64 v_lshl_add_u32"};
   unsigned long long* h = new unsigned long long[cus * kWaves];
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int v = 0; v < 8; ++v) {
+  for (int v = 0; v < 11; ++v) {
     hipLaunchKernelGGL(ks[v], dim3(cus), dim3(kWaves * 64), 0, 0, in, out, cyc, 100);
     hipDeviceSynchronize();
     hipEventRecord(e0);
