@@ -19,7 +19,7 @@ import sys
 
 KERNELS = {"k_sweep_flat": "plane_sweep", "k_score32": "ransac_score", "k_score": "ransac_score", "k_solve_front": "ransac_solve_front",
            "k_roots": "ransac_roots", "k_solve_back": "ransac_solve_back", "k_sweep": "plane_sweep", "k_solve": "ransac_solve",
-           "k_chain": "ransac_chain", "k_tgt_quads": "sweep_tgt_quads", "k_flow_points": "flow_to_points"}
+           "k_chain": "ransac_chain", "k_cand": "ransac_chain", "k_tgt_quads": "sweep_tgt_quads", "k_flow_points": "flow_to_points"}
 
 
 def kernel_key(name):
