@@ -4,9 +4,9 @@
 One step = one batch of `--batch` pairs per GPU through
     flow -> correspondences -> RANSAC five-point (H = 512 x iters)
     -> pose (RESCALE_DEPTH, NORM_TARGET 0.6) -> plane-sweep cost volume
-with every input already resident in HBM.  Consecutive steps overlap: each
-step's sweep runs on a side stream beside the next step's pose stage
-(``--no-pipeline``: one stream); the timed region ends after the last sweep.
+with every input already resident in HBM.  ``--pipeline`` overlaps
+consecutive steps (each step's sweep on a side stream beside the next step's
+pose stage); the timed region ends after the last sweep either way.
 ``--config`` picks the workload
 (BASELINE.json configs):
 
@@ -80,9 +80,10 @@ def parse(argv=None):
                     help="RANSAC reads the flow directly (sfm_ransac5_flow) instead of materialised correspondences")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-runs", type=int, default=3, help="full-pair CPU baseline runs (median)")
-    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
-                    help="one stream; by default each step's sweep runs on a side stream and overlaps the next "
-                         "step's pose stage (TwoViewHotPath.step_pipelined; c2 +1.7 %%, sparse +12 %%)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="each step's sweep on a side stream, overlapping the next step's pose stage "
+                         "(TwoViewHotPath.step_pipelined): c2 +1.7 %%, sparse +12 %% pairs/s, but the overlapped "
+                         "kernels' launch durations (the roofline fields) then include the overlap")
     args = ap.parse_args(argv)
     b, hw, it, nl, cd, kp = CONFIGS[args.config]
     args.batch = b if args.batch is None else args.batch
@@ -305,7 +306,7 @@ def _main_gpu(args, dist):
                         norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused,
                         keypoints=None if kp is None else (kp, [args.keypoints] * B))
 
-    # default: step i's sweep (side stream) overlaps step i+1's pose stage (--no-pipeline: one stream)
+    # --pipeline: step i's sweep (side stream) overlaps step i+1's pose stage
     stepf = hp.step_pipelined if args.pipeline else hp.step
     for _ in range(args.warmup):
         stepf(flow, K, ref_fea, tgt_fea)
