@@ -98,7 +98,10 @@ const TuneKey kTuneKeys[] = {
     {"sweep_lane_pixels", &sfm::Tuning::sweep_lane_pixels, [](int v) { return v >= 0 && v <= 2; }},
     {"sweep_items_per_block", &sfm::Tuning::sweep_items_per_block,
      [](int v) { return v == 1 || v == 2 || v == 4 || v == 8; }},
-    {"sweep_flat", &sfm::Tuning::sweep_flat, [](int v) { return v >= 0 && v <= 2; }},
+    {"sweep_flat", &sfm::Tuning::sweep_flat, [](int v) { return v >= 0 && v <= 3; }},
+    {"sweep_buffer", &sfm::Tuning::sweep_buffer, v_01},
+    {"sweep_run",&sfm::Tuning::sweep_run, [](int v) { return v >= 1 && v <= 1024; }},
+    {"sweep_band_rows", &sfm::Tuning::sweep_band_rows, [](int v) { return v >= 2 && v <= 64; }},
     {"sweep_nj", &sfm::Tuning::sweep_nj, [](int v) { return v == 1 || v == 2 || v == 4; }},
     {"sweep_group", &sfm::Tuning::sweep_group, [](int v) { return v == 4 || v == 8; }},
     {"score_blocks_per_cu", &sfm::Tuning::score_blocks_per_cu, v_1_64},

@@ -311,6 +311,8 @@ struct FlatGeom {
   int amask;       // elements per 256 bytes - 1
   int out_mis;     // element offset of the output pointer modulo amask + 1
   int pair_ok;     // bf16: every row starts at an even element (4-byte pair stores)
+  int buf_ok;      // k_sweep_tile fast path: per-pair volume, ref and quad ranges < 2^32 bytes, pair_ok
+  unsigned pair_bytes;   // one pair's output volume in bytes (buffer range)
   Magic mwin, mgrp, mhw;
   float inv_w;
   float dmax, dstep;
@@ -682,6 +684,131 @@ __device__ __forceinline__ void sweep_tile_item(const float* __restrict__ ref, c
   }
 }
 
+// Interior windows of a full channel group (the bulk of the volume), with
+// buffer addressing: one SGPR resource per pair and tensor, the per-lane
+// pixel byte offset in one VGPR shared by every row, each row's offset in an
+// SGPR (soffset).  The generic body above spends ~200 VALU per wave item on
+// 64-bit address arithmetic, partial-group branches and their zero moves
+// (SQ_INSTS_VALU 324 per item at KITTI, ~110 of them the sampling itself);
+// here stores and loads need no VALU address work.  Same arithmetic, so the
+// same bits.  Requires every per-pair byte range below 2^32 (g.buf_ok).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+template <typename OutT, int NQ, int NJ>
+__device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, const f32x4* __restrict__ tq,
+                                                const float* __restrict__ pose,
+                                                const float* __restrict__ K4, const float* __restrict__ K4inv,
+                                                const FlatGeom& g, OutT* __restrict__ out, int b, int k,
+                                                int start) {
+  constexpr bool BF = sizeof(OutT) == 2;
+  constexpr int G = 4 * NQ, WW = 64 * NJ;
+  const int c0 = k * G;
+  const int l0 = (int)magic_div((unsigned)start, g.mhw);
+  const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+  const int woff = start + WW * wave;
+  const int pbase = start - l0 * g.hw;
+  int ps[NJ], ls[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    int p = pbase + WW * wave + 64 * j + lane, l = l0;
+    if (g.hw >= 256 * NJ) {                    // a window spans at most two planes
+      if (p >= g.hw) { p -= g.hw; ++l; }
+    } else {
+      while (p >= g.hw) { p -= g.hw; ++l; }
+    }
+    ps[j] = p;
+    ls[j] = l;
+  }
+  const __amdgpu_buffer_rsrc_t rout = buf_rsrc(out + (size_t)b * g.rows * g.slab, g.pair_bytes);
+  const unsigned row_bytes = (unsigned)g.slab * (unsigned)sizeof(OutT);
+  float cp[G][NJ];
+  if (g.ref_rows) {
+    const __amdgpu_buffer_rsrc_t rref = buf_rsrc(ref + ((size_t)b * g.C + c0) * g.hw, (unsigned)G * g.hw * 4u);
+#pragma unroll
+    for (int c = 0; c < G; ++c)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        cp[c][j] = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(rref, (unsigned)ps[j] * 4u, (unsigned)c * g.hw * 4u, 0));
+  }
+  Proj pr;
+  load_proj(pose, K4, K4inv, b, pr);
+  const SampleK sk = sample_consts(g.h, g.w);
+  const float dA = plane_depth(g.dmax, g.dstep, l0), dB = plane_depth(g.dmax, g.dstep, l0 + 1);
+  const __amdgpu_buffer_rsrc_t rtq =
+      buf_rsrc(tq + ((size_t)b * g.C4 + k * NQ) * g.hw, (unsigned)NQ * g.hw * 16u);
+  f32x4 acc[NQ][NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int p = ps[j], l = ls[j];
+    float d = l == l0 ? dA : dB;
+    if (l > l0 + 1) d = plane_depth(g.dmax, g.dstep, l);
+    int y = (int)((float)p * g.inv_w);
+    int x = p - y * g.w;
+    if (x < 0) { --y; x += g.w; }
+    if (x >= g.w) { ++y; x -= g.w; }
+    const float xf = (float)x, yf = (float)y;
+    float ray[3];
+    ray[0] = (pr.ki[0] * xf + pr.ki[1] * yf) + pr.ki[2];
+    ray[1] = (pr.ki[3] * xf + pr.ki[4] * yf) + pr.ki[5];
+    ray[2] = (pr.ki[6] * xf + pr.ki[7] * yf) + pr.ki[8];
+    float ix, iy;
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) acc[n][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (sample_pos_nr(pr, ray, d, sk, ix, iy)) {
+      TapsIn tp;
+      make_taps_inside(ix, iy, g.h, g.w, tp);
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        const unsigned so = (unsigned)n * g.hw * 16u;
+        f32x4 t[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          t[e] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtq, tp.off[e] * 16u, so, 0));
+        f32x4 a;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = tp.wt[0] * t[0][e];
+          v = __builtin_fmaf(tp.wt[1], t[1][e], v);
+          v = __builtin_fmaf(tp.wt[2], t[2][e], v);
+          a[e] = __builtin_fmaf(tp.wt[3], t[3][e], v);
+        }
+        acc[n][j] = a;
+      }
+    }
+  }
+  const bool odd = (lane & 1) != 0;
+  // row r of the pair: soffset r * row_bytes; per-lane byte offset(s) of the window
+  auto store_row = [&](unsigned r, const float* v) {
+    const unsigned so = r * row_bytes;
+    if (!BF) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), rout, (unsigned)(woff + 64 * j + lane) * 4u, so, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < NJ / 2; ++s) {
+        const unsigned u = bf16_pair_swap(to_bf16(v[2 * s]), to_bf16(v[2 * s + 1]), odd);
+        const int f = woff + 128 * s + lane + (odd ? 63 : 0);
+        __builtin_amdgcn_raw_buffer_store_b32(u, rout, (unsigned)f * 2u, so, 0);
+      }
+    }
+  };
+  if (g.ref_rows) {
+#pragma unroll
+    for (int c = 0; c < G; ++c) store_row((unsigned)(c0 + c), cp[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < G; ++c) {
+    float v[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) v[j] = acc[c >> 2][j][c & 3];
+    store_row((unsigned)(g.ref_rows + c0 + c), v);
+  }
+}
+
 template <typename OutT, int NQ, int NJ>
 __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restrict__ ref,
                                                            const f32x4* __restrict__ tq,
@@ -698,7 +825,9 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
   const size_t wbase = ((size_t)b * g.rows + g.ref_rows + k * 4 * NQ) * (size_t)g.slab;
   const int start = win * WIN - (int)((wbase + (size_t)g.out_mis) & (size_t)g.amask);
   if (start >= g.slab) return;
-  if (start >= 0 && start + WIN <= g.slab)
+  if (g.buf_ok && start >= 0 && start + WIN <= g.slab && (k + 1) * 4 * NQ <= g.C)
+    sweep_tile_fast<OutT, NQ, NJ>(ref, tq, pose, K4, K4inv, g, out, b, k, start);
+  else if (start >= 0 && start + WIN <= g.slab)
     sweep_tile_item<OutT, NQ, NJ, true>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
   else
     sweep_tile_item<OutT, NQ, NJ, false>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
@@ -725,6 +854,252 @@ static void launch_k_sweep_flat(int nq, unsigned blocks, hipStream_t s, const fl
   else
     hipLaunchKernelGGL((k_sweep_flat<OutT, 1>), dim3(blocks), dim3(kSwThreads), 0, s, ref, tq, pose, K4, K4inv, g,
                        (OutT*)out);
+}
+
+// ---------------------------------------------------------------------------
+// Cost volume, plane-run form with the target band in LDS (sweep_flat = 3).
+//
+// k_sweep_tile is bound by the texture address/data units, not by HBM: per
+// pixel and channel quad a lane issues four 16-byte tap gathers (64 B through
+// the L1 path for 16 B of output), and re-reads the same target pixels at
+// every plane (PMC: 1.8 GB of reads per launch against 0.06 GB algorithmic).
+// Here one block produces a run of R consecutive planes of one 256*NJ-pixel
+// tile for one channel quad:
+//   * the source rows every tap of the run touches are found first (the same
+//     sample positions, computed twice), and that band of full target rows --
+//     contiguous in tq -- is copied once into LDS; the taps are then ds_read
+//     from it (lanes whose taps fall outside a band clipped to the LDS budget
+//     gather from global memory, same values);
+//   * the tile's reference pixels (the same at every plane) are staged once
+//     and stored R times;
+//   * the windows stay 256-byte aligned per plane: at plane l the tile covers
+//     pixels [WIN n - ph_l, WIN n - ph_l + WIN), ph_l the row's misalignment
+//     at that plane, so every full wave store is one aligned segment.
+// On KITTI (94x311 features, |t| 0.6) the band of a 16-plane run is 6 rows at
+// the median, 14 at p99: ~15 B of staged reads per 4 channels of a pixel
+// and plane instead of 64 B of gathers.  Same arithmetic as k_sweep_tile
+// (bit-identical volumes).
+// ---------------------------------------------------------------------------
+struct BandGeom {
+  int C, C4, h, w, hw, L;
+  int ref_rows, rows;
+  int slab;        // L * hw elements
+  int ntiles;      // tiles per plane: ceil((hw + A - 1) / WIN)
+  int nruns;       // plane runs per quad: ceil(L / run)
+  int run;         // planes per block
+  int amask;       // A - 1, A = elements per 256 bytes
+  int out_mis;     // element offset of the output pointer modulo A
+  int hwmod;       // hw mod A
+  int pair_ok;     // bf16: every row starts at an even element
+  int cap_rows;    // band rows the LDS holds
+  Magic mtile, mrun, mgrp;
+  float inv_w, dmax, dstep;
+};
+
+template <int NJ>
+__device__ __forceinline__ int band_pixel(int ws, int wave, int lane, int j) {
+  return ws + 64 * NJ * wave + 64 * j + lane;
+}
+
+constexpr int kBandThreads = 1024;   // 16 waves: 4 wave groups x 4 waves over the tile
+
+template <typename OutT, int NJ>
+__global__ __launch_bounds__(kBandThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_band(const float* __restrict__ ref,
+                                                             const f32x4* __restrict__ tq,
+                                                             const float* __restrict__ pose,
+                                                             const float* __restrict__ K4,
+                                                             const float* __restrict__ K4inv, BandGeom g,
+                                                             OutT* __restrict__ out) {
+  constexpr bool BF = sizeof(OutT) == 2;
+  static_assert(!BF || NJ % 2 == 0, "bf16 windows pack register pairs");
+  constexpr int WIN = 256 * NJ;
+  extern __shared__ f32x4 s_band[];            // cap_rows * w quads, then the reference tile
+  __shared__ int s_ylo, s_yhi;
+  const unsigned item = blockIdx.x;            // ((b * C4 + k) * nruns + run) * ntiles + n
+  const unsigned r1 = magic_div(item, g.mtile);
+  const int n = (int)(item - r1 * (unsigned)g.ntiles);
+  const unsigned r2 = magic_div(r1, g.mrun);
+  const int run = (int)(r1 - r2 * (unsigned)g.nruns);
+  const int b = (int)magic_div(r2, g.mgrp);
+  const int k = (int)(r2 - (unsigned)b * (unsigned)g.C4);
+  const int tid = (int)threadIdx.x;
+  const int lane = tid & 63, wave = (tid >> 6) & 3, grp = tid >> 8;   // wave group grp takes planes l0 + grp + 4 i
+  const int A = g.amask + 1;
+  const int l0 = run * g.run, l1 = min(g.L, l0 + g.run);
+  const int nc = min(4, g.C - 4 * k);
+  const size_t wrow = ((size_t)b * g.rows + g.ref_rows + 4 * k) * (size_t)g.slab;   // first warped row
+  const int wmis = (int)((wrow + (size_t)g.out_mis) & (size_t)g.amask);
+  auto phase = [&](int l) { return (wmis + (int)(((unsigned)l * (unsigned)g.hwmod) & (unsigned)g.amask)) & g.amask; };
+  const int rbase = WIN * n - A;               // reference tile: pixels [rbase, rbase + WIN + A)
+  const int RW = WIN + A;                      // <= 640 < kBandThreads
+  float* s_ref = reinterpret_cast<float*>(s_band + g.cap_rows * g.w);
+
+  if (tid == 0) { s_ylo = 0x7fffffff; s_yhi = -1; }
+  // reference tile loads first: in flight during the band estimate
+  float rv[4];
+  if (g.ref_rows) {
+    const int p = rbase + tid;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float* R = ref + ((size_t)b * g.C + 4 * k + min(c, nc - 1)) * g.hw;
+      rv[c] = (tid < RW && p >= 0 && p < g.hw) ? R[p] : 0.0f;
+    }
+  }
+  Proj pr;
+  load_proj(pose, K4, K4inv, b, pr);
+  const SampleK sk = sample_consts(g.h, g.w);
+  auto pixel_ray = [&](int p, float (&ray)[3]) {
+    int y = (int)((float)p * g.inv_w);
+    int x = p - y * g.w;
+    if (x < 0) { --y; x += g.w; }
+    if (x >= g.w) { ++y; x -= g.w; }
+    const float xf = (float)x, yf = (float)y;
+    ray[0] = (pr.ki[0] * xf + pr.ki[1] * yf) + pr.ki[2];
+    ray[1] = (pr.ki[3] * xf + pr.ki[4] * yf) + pr.ki[5];
+    ray[2] = (pr.ki[6] * xf + pr.ki[7] * yf) + pr.ki[8];
+  };
+
+  // Band estimate: the tap rows of the tile at four planes of the run (its
+  // first and last, and two between; one per wave group).  A pixel's sample
+  // moves monotonically along its epipolar line with the plane, so the run's
+  // taps lie between the end planes' almost everywhere; the exceptions (and
+  // bands clipped to cap_rows) take the global path below, so the estimate
+  // changes only speed, never values.
+  int ylo = 0x7fffffff, yhi = -1;
+  {
+    const int l = l0 + (grp * (l1 - 1 - l0) + 1) / 3;
+    const float d = plane_depth(g.dmax, g.dstep, l);
+    const int ws = WIN * n - phase(l);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int p = band_pixel<NJ>(ws, wave, lane, j);
+      if (p >= 0 && p < g.hw) {
+        float ray[3], ix, iy;
+        pixel_ray(p, ray);
+        if (sample_pos_nr(pr, ray, d, sk, ix, iy)) {
+          const int y0 = (int)floorf(iy);
+          ylo = min(ylo, y0);
+          yhi = max(yhi, y0 + (y0 < g.h - 1 ? 1 : 0));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    ylo = min(ylo, __shfl_xor(ylo, o));
+    yhi = max(yhi, __shfl_xor(yhi, o));
+  }
+  __syncthreads();   // s_ylo / s_yhi initialised
+  if (lane == 0) { atomicMin(&s_ylo, ylo); atomicMax(&s_yhi, yhi); }
+  if (g.ref_rows && tid < RW) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s_ref[c * RW + tid] = rv[c];
+  }
+  __syncthreads();
+  int by0 = s_ylo, nb = 0;
+  if (s_yhi >= by0) {
+    // a little slack around the estimate, inside the image and the LDS
+    const int want_lo = max(by0 - 1, 0), want_hi = min(s_yhi + 1, g.h - 1);
+    nb = min(want_hi - want_lo + 1, g.cap_rows);
+    by0 = want_lo;
+  } else {
+    by0 = 0;
+  }
+  const f32x4* T = tq + ((size_t)b * g.C4 + k) * g.hw;   // this quad's target plane
+  {
+    const f32x4* src = T + (size_t)by0 * g.w;
+    const int cnt = nb * g.w;
+    int i = tid;
+    for (; i + kBandThreads < cnt; i += 2 * kBandThreads) {
+      const f32x4 a0 = src[i], a1 = src[i + kBandThreads];
+      s_band[i] = a0; s_band[i + kBandThreads] = a1;
+    }
+    if (i < cnt) s_band[i] = src[i];
+  }
+  __syncthreads();
+  const unsigned lo = (unsigned)(by0 * g.w), span = (unsigned)(nb * g.w);
+  const bool odd = (lane & 1) != 0;
+
+  for (int l = l0 + grp; l < l1; l += 4) {
+    const float d = plane_depth(g.dmax, g.dstep, l);
+    const int ws = WIN * n - phase(l);
+    const int fl = l * g.hw;                   // slab index of the plane's pixel 0
+    float acc[4][NJ], cp[4][NJ];
+    bool ok[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int p = band_pixel<NJ>(ws, wave, lane, j);
+      ok[j] = p >= 0 && p < g.hw;
+      const int pp = ok[j] ? p : max(rbase, 0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        acc[c][j] = 0.0f;
+        cp[c][j] = g.ref_rows ? s_ref[c * RW + (pp - rbase)] : 0.0f;
+      }
+      float ray[3], ix, iy;
+      pixel_ray(pp, ray);
+      if (ok[j] && sample_pos_nr(pr, ray, d, sk, ix, iy)) {
+        TapsIn tp;
+        make_taps_inside(ix, iy, g.h, g.w, tp);
+        f32x4 t0, t1, t2, t3;
+        if (tp.off[0] - lo < span && tp.off[3] - lo < span) {
+          t0 = s_band[tp.off[0] - lo]; t1 = s_band[tp.off[1] - lo];
+          t2 = s_band[tp.off[2] - lo]; t3 = s_band[tp.off[3] - lo];
+        } else {
+          t0 = *at_u32(T, tp.off[0] * 16u); t1 = *at_u32(T, tp.off[1] * 16u);
+          t2 = *at_u32(T, tp.off[2] * 16u); t3 = *at_u32(T, tp.off[3] * 16u);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = tp.wt[0] * t0[e];
+          v = __builtin_fmaf(tp.wt[1], t1[e], v);
+          v = __builtin_fmaf(tp.wt[2], t2[e], v);
+          acc[e][j] = __builtin_fmaf(tp.wt[3], t3[e], v);
+        }
+      }
+    }
+    auto store_row = [&](OutT* row, const float* v) {
+      if (!BF) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int p = band_pixel<NJ>(ws, wave, lane, j);
+          if (ok[j]) store1(at_u32(row, (unsigned)(fl + p) * 4u), v[j]);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < NJ / 2; ++s) {
+          const unsigned a = to_bf16(v[2 * s]), bb = to_bf16(v[2 * s + 1]);
+          const unsigned u = bf16_pair_swap(a, bb, odd);
+          // even lane 2m: pixels 128 s + 2m, +1; odd lane 2m+1: 128 s + 64 + 2m, +1
+          const int p = ws + 64 * NJ * wave + 128 * s + lane + (odd ? 63 : 0);
+          const bool okl = p >= 0 && p < g.hw, okh = p + 1 >= 0 && p + 1 < g.hw;
+          if (g.pair_ok && okl && okh) {
+            *reinterpret_cast<unsigned int*>(at_u32(row, (unsigned)(fl + p) * 2u)) = u;
+          } else {
+            if (okl) row[fl + p] = (unsigned short)(u & 0xffffu);
+            if (okh) row[fl + p + 1] = (unsigned short)(u >> 16);
+          }
+        }
+      }
+    };
+    if (g.ref_rows) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= nc) break;
+        store_row(out + ((size_t)b * g.rows + 4 * k + c) * (size_t)g.slab, cp[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c >= nc) break;
+      store_row(out + wrow + (size_t)c * g.slab, acc[c]);
+    }
+  }
+}
+
+// LDS bytes of one k_sweep_band block holding `rows` band rows
+static size_t band_lds_bytes(int rows, int w, int nj) {
+  return (size_t)rows * w * sizeof(f32x4) + 4 * (size_t)(256 * nj + 128) * sizeof(float);   // band + ref tile
 }
 
 // inverse_warp for an arbitrary depth map (models/inverse_warp.py:121-153)
@@ -840,6 +1215,49 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   // k_sweep_tile: 256 * nj elements per window (bf16 packs register pairs: nj even)
   int nj = tuning().sweep_nj;
   if (out_dtype == 1 && nj < 2) nj = 2;
+  if (mode == 3 && hw < (1 << 24) && slab < ((int64_t)1 << 30)) {
+    const int bnj = out_dtype == 1 ? 2 : 1;
+    const int esz = out_dtype == 0 ? 4 : 2;
+    BandGeom bg;
+    bg.C = C; bg.C4 = g.C4; bg.h = h; bg.w = w; bg.hw = hw; bg.L = L;
+    bg.ref_rows = g.ref_rows; bg.rows = g.rows; bg.slab = (int)slab;
+    bg.amask = 256 / esz - 1;
+    bg.ntiles = (hw + bg.amask + 256 * bnj - 1) / (256 * bnj);
+    bg.run = std::min(tuning().sweep_run, L);
+    bg.nruns = (L + bg.run - 1) / bg.run;
+    bg.out_mis = (int)(((uintptr_t)out / esz) & (uintptr_t)bg.amask);
+    bg.hwmod = hw & bg.amask;
+    bg.pair_ok = (slab % 2 == 0) && ((uintptr_t)out % 4 == 0);
+    // two blocks per CU: <= 80 KB of LDS each
+    const size_t lds_cap = 80 * 1024 - 64;
+    const size_t row_bytes = (size_t)w * sizeof(f32x4);
+    const size_t fixed = band_lds_bytes(0, w, bnj);
+    const int rows_fit = lds_cap > fixed ? (int)((lds_cap - fixed) / row_bytes) : 0;
+    bg.cap_rows = std::min(std::min(tuning().sweep_band_rows, rows_fit), h);
+    const int64_t nblk = (int64_t)B * g.C4 * bg.nruns * bg.ntiles;
+    if (bg.cap_rows >= 2 && nblk < ((int64_t)1 << 31)) {
+      bg.mtile = make_magic((unsigned)bg.ntiles);
+      bg.mrun = make_magic((unsigned)bg.nruns);
+      bg.mgrp = make_magic((unsigned)bg.C4);
+      bg.inv_w = 1.0f / (float)w;
+      bg.dmax = g.dmax; bg.dstep = g.dstep;
+      const unsigned lds = (unsigned)band_lds_bytes(bg.cap_rows, w, bnj);
+      ProfScope ps(pname, s);
+      if (out_dtype == 0) {
+        SFM_HIP(hipFuncSetAttribute((const void*)k_sweep_band<float, 1>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((k_sweep_band<float, 1>), dim3((unsigned)nblk), dim3(kBandThreads), lds, s, ref, tq, pose,
+                           K4, K4inv, bg, (float*)out);
+      } else {
+        SFM_HIP(hipFuncSetAttribute((const void*)k_sweep_band<unsigned short, 2>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((k_sweep_band<unsigned short, 2>), dim3((unsigned)nblk), dim3(kBandThreads), lds, s, ref,
+                           tq, pose, K4, K4inv, bg, (unsigned short*)out);
+      }
+      SFM_LAUNCHED();
+      return SFM_OK;
+    }
+  }
   const int64_t win_el = mode == 2 ? 256 * (int64_t)nj : kFlatWin;
   const int64_t nwin = (slab + 127 + win_el - 1) / win_el;
   if (mode && hw < (1 << 24) && slab < ((int64_t)1 << 30) && (int64_t)B * fgroups * nwin < ((int64_t)1 << 31)) {
@@ -851,6 +1269,9 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     fg.amask = 256 / esz - 1;
     fg.out_mis = (int)(((uintptr_t)out / esz) & (uintptr_t)fg.amask);
     fg.pair_ok = (slab % 2 == 0) && ((uintptr_t)out % 4 == 0);
+    const int64_t pair_bytes = (int64_t)g.rows * slab * esz;
+    fg.buf_ok = pair_bytes < ((int64_t)1 << 32) && (out_dtype == 0 || fg.pair_ok) && tuning().sweep_buffer;
+    fg.pair_bytes = fg.buf_ok ? (unsigned)pair_bytes : 0u;
     fg.mwin = make_magic((unsigned)nwin);
     fg.mgrp = make_magic((unsigned)fgroups);
     fg.mhw = make_magic((unsigned)hw);

@@ -288,6 +288,10 @@ int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int chann
  *     "sweep_lane_pixels"     0..2    pixel-to-lane mapping of the per-row sweep (0)
  *     "sweep_items_per_block" 1,2,4,8 work items per block of the per-row sweep (4)
  *     "sweep_nj"              1,2,4   pixels per lane of k_sweep_tile (1; bf16 uses 2)
+ *     "sweep_buffer"          0, 1    buffer-addressed interior path of k_sweep_tile (1)
+ *     "sweep_run"             1..1024 planes per block of k_sweep_band (16)
+ *     "sweep_band_rows"       2..64   target rows k_sweep_band stages in LDS (16,
+ *                                     clipped to 80 KB per block)
  *     "score_blocks_per_cu"   1..64   persistent k_score32 blocks per CU (32)
  *     "score_mf_blocks_per_cu" 1..8   persistent k_score_mf blocks per CU (1)
  *     "score_prune"           0, 1    exact bound pruning in k_score32 (1; winner,
@@ -301,8 +305,10 @@ int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int chann
  *     "conv_rolling"          0, 1    rolling-plane Conv3d for cin 32 (1; same bits)
  *
  *   results MAY change (sweep outputs by FMA rounding only):
- *     "sweep_flat"            0, 1, 2 2 (default): k_sweep_tile, 1: k_sweep_flat
- *                                     (the two are bit-identical); both sum the
+ *     "sweep_flat"            0..3    2 (default): k_sweep_tile, 1: k_sweep_flat,
+ *                                     3: k_sweep_band (plane runs, target band in
+ *                                     LDS; measured slower); 1-3 are bit-identical
+ *                                     to each other; they sum the
  *                                     four bilinear taps with FMA, which differs
  *                                     from 0, the per-row kernel in the
  *                                     reference's mul/add order, by <= 7.2e-7

@@ -3,7 +3,10 @@ k_sweep_flat, sweep_flat=1) against the per-row kernel (sweep_flat=0) and the
 oracle: both group sizes, every window width of k_sweep_tile (bit-identical to
 k_sweep_flat of the same group),
 edge windows, feature maps under one 1024-pixel window, odd slabs and output
-pointers off the 256-byte grid.  Sample positions are bit-identical
+pointers off the 256-byte grid; and the plane-run kernel k_sweep_band
+(sweep_flat=3: target band in LDS, bit-identical to k_sweep_tile) at several
+run lengths and LDS band heights, down to a 2-row band whose taps mostly take
+the global-gather path.  Sample positions are bit-identical
 (warp.h sample_pos_nr); the 4-tap sum differs by FMA rounding only."""
 import pytest
 import torch
@@ -37,18 +40,32 @@ def test_aligned_slab_kernels_match_per_row(cuda, B, C, L, h, w, dtype, offset):
     outs = {}
     try:
         for flat, group, nj in ((0, 4, 1), (1, 4, 1), (1, 8, 1), (2, 4, 1), (2, 4, 2), (2, 4, 4),
-                                (2, 8, 1), (2, 8, 2), (2, 8, 4)):
+                                (2, 8, 1), (2, 8, 2), (2, 8, 4),
+                                # k_sweep_band: (3, planes per block, LDS band rows); 2 rows
+                                # sends most taps down the global-gather path
+                                (3, 16, 16), (3, 3, 16), (3, 1, 2), (3, 5, 3),
+                                # k_sweep_tile without its buffer-addressed interior path
+                                (2, 8, -1), (2, 4, -2)):
             _lib.tune("sweep_flat", flat)
-            _lib.tune("sweep_group", group)
-            _lib.tune("sweep_nj", nj)
+            _lib.tune("sweep_buffer", 0 if nj < 0 else 1)
+            nj = abs(nj)
+            if flat == 3:
+                _lib.tune("sweep_run", group)
+                _lib.tune("sweep_band_rows", nj)
+            else:
+                _lib.tune("sweep_group", group)
+                _lib.tune("sweep_nj", nj)
             buf = torch.full((n + offset,), float("nan"), dtype=dtype, device=cuda)
             out = buf[offset:].view(B, 2 * C, L, h, w)
             plane_sweep_cost(*args, dtype=dtype, out=out)
-            outs[(flat, group, nj)] = out.float().cpu()
+            outs[(flat, group, nj) if _lib.tune_get("sweep_buffer") else (flat, group, -nj)] = out.float().cpu()
     finally:
         _lib.tune("sweep_flat", 2)
         _lib.tune("sweep_group", 8)
         _lib.tune("sweep_nj", 1)
+        _lib.tune("sweep_run", 16)
+        _lib.tune("sweep_band_rows", 16)
+        _lib.tune("sweep_buffer", 1)
     base = outs[(0, 4, 1)]
     assert not torch.isnan(base).any()
     tol = 2e-6 if dtype == torch.float32 else 1e-2
@@ -60,8 +77,46 @@ def test_aligned_slab_kernels_match_per_row(cuda, B, C, L, h, w, dtype, offset):
         assert float((got - base).abs().max()) <= tol, (key, float((got - base).abs().max()))
         if key[0] == 2:                                   # same arithmetic as k_sweep_flat
             assert torch.equal(got, outs[(1, key[1], 1)]), key
+        if key[0] == 3 or key[2] < 0:                     # same arithmetic as k_sweep_tile
+            assert torch.equal(got, outs[(2, 8, 1)]), key
     if dtype == torch.float32:
         want = S.plane_sweep_cost(ref, tgt, pose, K, Ki, L, 0.8)
         got = outs[(2, 8, 1)]
         err = (got - want).abs() - RTOL * torch.clamp(want.abs(), min=FLOOR)
         assert float(err.max()) <= 0.0, float((got - want).abs().max())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("run,rows", [(16, 16), (32, 6), (128, 16)])
+def test_band_kernel_full_size_kitti(cuda, dtype, run, rows):
+    """k_sweep_band at the bench's volume (94x311, L=128, C=32, B=2, translation
+    scaled to 0.6 as the bench's RESCALE_DEPTH pose): bit-identical to
+    k_sweep_tile for run lengths whose bands fit the LDS and ones that do not
+    (6 rows, a 128-plane run: clipped bands, global gathers for the rest)."""
+    from sfm_amd import _lib, synth
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
+    B, C, L = 2, 32, 128
+    h, w = synth.feature_hw()
+    ref, tgt = synth.features(B, C, h, w, seed=11)
+    K = synth.intrinsics(B)
+    Ki = torch.inverse(K)
+    pose = synth.relative_pose(B, torch.Generator().manual_seed(3))
+    pose[:, :, 3] *= 0.6 / pose[:, :, 3].norm(dim=1, keepdim=True)
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    args = (ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 1.0)
+    try:
+        _lib.tune("sweep_flat", 2)
+        want = plane_sweep_cost(*args, dtype=dtype)
+        _lib.tune("sweep_buffer", 0)                  # the generic k_sweep_tile body
+        assert torch.equal(plane_sweep_cost(*args, dtype=dtype), want)
+        _lib.tune("sweep_buffer", 1)
+        _lib.tune("sweep_flat", 3)
+        _lib.tune("sweep_run", run)
+        _lib.tune("sweep_band_rows", rows)
+        got = plane_sweep_cost(*args, dtype=dtype)
+    finally:
+        _lib.tune("sweep_flat", 2)
+        _lib.tune("sweep_run", 16)
+        _lib.tune("sweep_band_rows", 16)
+    assert torch.equal(got, want)
+    assert float(want[:, C:].float().abs().sum()) > 0.0
