@@ -19,7 +19,7 @@ K4, Ki4 = SW.quarter_intrinsics(K, torch.inverse(K))
 P = pose[:, :3, :4].float().clone()
 P[:, :, 3] *= 0.6 / P[:, :, 3].norm(dim=1, keepdim=True)
 P = P.contiguous().to(dev)
-variants = [(2, 0, 0), (2, 0, 1)] + [(3, r, rows) for r in (int(x) for x in os.environ.get("RUNS", "").split(",") if x)
+variants = [(2, 0, 0), (2, 0, 1), (2, -2, 1)] + [(3, r, rows) for r in (int(x) for x in os.environ.get("RUNS", "").split(",") if x)
                                     for rows in (int(x) for x in os.environ.get("ROWS", "16").split(","))]
 res = {}
 
@@ -44,6 +44,8 @@ for dt in (torch.float32, torch.bfloat16):
             _lib.tune("sweep_buffer", rows if flat == 2 else 1)
             if flat == 3:
                 _lib.tune("sweep_run", r); _lib.tune("sweep_band_rows", rows)
+            else:   # run = -nj (pixels per lane)
+                _lib.tune("sweep_nj", -r if r < 0 else 1)
             out.fill_(7.0)
             res.setdefault(f"{str(dt)[6:]} flat={flat} run={r} rows={rows}", []).append(timed("plane_sweep", run))
             if rnd == 0 and not torch.equal(out, want):
@@ -51,7 +53,8 @@ for dt in (torch.float32, torch.bfloat16):
                 print(f"MISMATCH {dt} flat={flat} run={r} rows={rows}: max|diff| {float(d.max()):.3g} "
                       f"n={int((d > 0).sum())}", flush=True)
     del out, want
-_lib.tune("sweep_flat", 2); _lib.tune("sweep_buffer", 1); _lib.tune("sweep_run", 16); _lib.tune("sweep_band_rows", 16)
+_lib.tune("sweep_flat", 2); _lib.tune("sweep_buffer", 1); _lib.tune("sweep_nj", 1)
+_lib.tune("sweep_run", 16); _lib.tune("sweep_band_rows", 16)
 for k, v in res.items():
     gb = B * 2 * C * L * h * w * (4 if "float32" in k else 2) / 1e9 + B * 2 * C * h * w * 4 / 1e9
     med = sorted(v)[len(v) // 2]
