@@ -42,10 +42,29 @@ constexpr int kSwWin = kSwThreads * kSwPix;
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-// tgt [B][C][hw] -> tq [B][C4][hw] float4 (channels >= C are zero)
-__global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4, int hw, f32x4* __restrict__ tq) {
+__device__ __forceinline__ float plane_depth(float dmax, float dstep, int l) {
+  // PSNet.py:150-153: depth planes (i+1)*MIN_DEPTH, or disp2depth / (i+1)
+  return dstep > 0.0f ? (float)(l + 1) * dstep : dmax / (float)(l + 1);
+}
+
+// tgt [B][C][hw] -> tq [B][C4][hw] float4 (channels >= C are zero).  With
+// `projs`, threads 0..B-1 also write each pair's Proj (K.pose rows and K^-1,
+// load_proj's float32 expression order), so the sweep's waves read it with
+// scalar loads instead of each recomputing the uniform 3x3.3x4 product on the
+// VALU (~80 instructions per wave item); threads 0..L-1 the plane depths
+// (two IEEE divisions per wave item otherwise).
+__global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4, int hw, f32x4* __restrict__ tq,
+                            const float* __restrict__ pose, const float* __restrict__ K4,
+                            const float* __restrict__ K4inv, Proj* __restrict__ projs, int L, float dmax,
+                            float dstep, float* __restrict__ depths) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)B * C4 * hw;
+  if (projs && i < B) {
+    Proj pr;
+    load_proj(pose, K4, K4inv, (int)i, pr);
+    projs[i] = pr;
+  }
+  if (depths && i < L) depths[i] = plane_depth(dmax, dstep, (int)i);
   if (i >= total) return;
   const int p = (int)(i % hw);
   const int64_t bq = i / hw;
@@ -62,7 +81,8 @@ __global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4,
 void launch_channel_quads(const float* feat, int B, int C, int hw, f32x4* quads, hipStream_t s) {
   const int C4 = (C + 3) / 4;
   const int64_t n = (int64_t)B * C4 * hw;
-  hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, feat, B, C, C4, hw, quads);
+  hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, feat, B, C, C4, hw, quads,
+                     nullptr, nullptr, nullptr, nullptr, 0, 0.0f, 0.0f, nullptr);
 }
 
 __device__ __forceinline__ void store4(float* dst, const float (&v)[4]) {
@@ -316,16 +336,13 @@ struct FlatGeom {
   Magic mwin, mgrp, mhw;
   float inv_w;
   float dmax, dstep;
+  const float* depths;   // plane depths (k_tgt_quads), or null
 };
 
 template <typename OutT> struct FlatLanes;   // pixels per lane per store, stores per lane per row
 template <> struct FlatLanes<float> { static constexpr int PXL = 1, NS = 4; };
 template <> struct FlatLanes<unsigned short> { static constexpr int PXL = 2, NS = 2; };
 
-__device__ __forceinline__ float plane_depth(float dmax, float dstep, int l) {
-  // PSNet.py:150-153: depth planes (i+1)*MIN_DEPTH, or disp2depth / (i+1)
-  return dstep > 0.0f ? (float)(l + 1) * dstep : dmax / (float)(l + 1);
-}
 
 template <typename OutT, int PXL>
 __device__ __forceinline__ void store_px(OutT* row, int f0, int slab, bool pair_ok, const float* v) {
@@ -698,10 +715,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uns
 
 template <typename OutT, int NQ, int NJ>
 __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, const f32x4* __restrict__ tq,
-                                                const float* __restrict__ pose,
-                                                const float* __restrict__ K4, const float* __restrict__ K4inv,
-                                                const FlatGeom& g, OutT* __restrict__ out, int b, int k,
-                                                int start) {
+                                                const Proj* __restrict__ projs, const FlatGeom& g,
+                                                OutT* __restrict__ out, int b, int k, int start) {
   constexpr bool BF = sizeof(OutT) == 2;
   constexpr int G = 4 * NQ, WW = 64 * NJ;
   const int c0 = k * G;
@@ -733,10 +748,16 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
         cp[c][j] = __uint_as_float(
             __builtin_amdgcn_raw_buffer_load_b32(rref, (unsigned)ps[j] * 4u, (unsigned)c * g.hw * 4u, 0));
   }
-  Proj pr;
-  load_proj(pose, K4, K4inv, b, pr);
+  const Proj pr = projs[b];                    // uniform: scalar loads
   const SampleK sk = sample_consts(g.h, g.w);
-  const float dA = plane_depth(g.dmax, g.dstep, l0), dB = plane_depth(g.dmax, g.dstep, l0 + 1);
+  float dA, dB;
+  if (g.depths) {
+    dA = g.depths[l0];
+    dB = l0 + 1 < g.L ? g.depths[l0 + 1] : dA;
+  } else {
+    dA = plane_depth(g.dmax, g.dstep, l0);
+    dB = plane_depth(g.dmax, g.dstep, l0 + 1);
+  }
   const __amdgpu_buffer_rsrc_t rtq =
       buf_rsrc(tq + ((size_t)b * g.C4 + k * NQ) * g.hw, (unsigned)NQ * g.hw * 16u);
   f32x4 acc[NQ][NJ];
@@ -815,7 +836,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
                                                            const float* __restrict__ pose,
                                                            const float* __restrict__ K4,
                                                            const float* __restrict__ K4inv, FlatGeom g,
-                                                           OutT* __restrict__ out) {
+                                                           OutT* __restrict__ out, const Proj* __restrict__ projs) {
   constexpr int WIN = 256 * NJ;
   const unsigned item = blockIdx.x;            // grid = B * groups * nwin
   const unsigned r = magic_div(item, g.mwin);
@@ -826,7 +847,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
   const int start = win * WIN - (int)((wbase + (size_t)g.out_mis) & (size_t)g.amask);
   if (start >= g.slab) return;
   if (g.buf_ok && start >= 0 && start + WIN <= g.slab && (k + 1) * 4 * NQ <= g.C)
-    sweep_tile_fast<OutT, NQ, NJ>(ref, tq, pose, K4, K4inv, g, out, b, k, start);
+    sweep_tile_fast<OutT, NQ, NJ>(ref, tq, projs, g, out, b, k, start);
   else if (start >= 0 && start + WIN <= g.slab)
     sweep_tile_item<OutT, NQ, NJ, true>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
   else
@@ -836,12 +857,16 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
 template <typename OutT, int NQ>
 static void launch_k_sweep_tile_nj(int nj, unsigned blocks, hipStream_t s, const float* ref, const f32x4* tq,
                                    const float* pose, const float* K4, const float* K4inv, const FlatGeom& g,
-                                   void* out) {
+                                   void* out, const Proj* projs) {
   const dim3 grid(blocks), block(kSwThreads);
   constexpr bool BF = sizeof(OutT) == 2;
-  if (nj >= 4) hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, 4>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
-  else if (nj == 2 || BF) hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, 2>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
-  else hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, (BF ? 2 : 1)>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out);
+  if (nj >= 4)
+    hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, 4>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out, projs);
+  else if (nj == 2 || BF)
+    hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, 2>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out, projs);
+  else
+    hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, (BF ? 2 : 1)>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g,
+                       (OutT*)out, projs);
 }
 
 template <typename OutT>
@@ -1163,9 +1188,15 @@ static void launch_k_sweep(int ipb, int64_t blocks, hipStream_t s, const float* 
 }
 
 // workspace: channel quads tq [B][C4][hw] float4
-static size_t sweep_ws_bytes(int B, int C, int h, int w) {
+static size_t sweep_quads_bytes(int B, int C, int h, int w) {
   const int C4 = (C + 3) / 4;
   return (size_t)B * C4 * (size_t)h * w * sizeof(f32x4);
+}
+// workspace: channel quads, then the per-pair Proj table
+constexpr int kDepthTable = 1024;   // plane depths kept in the workspace for L <= this
+static size_t sweep_proj_bytes(int B) { return ((size_t)B * sizeof(Proj) + 255) & ~(size_t)255; }
+static size_t sweep_ws_bytes(int B, int C, int h, int w) {
+  return sweep_quads_bytes(B, C, h, w) + sweep_proj_bytes(B) + kDepthTable * sizeof(float);
 }
 
 static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B, int C, int h, int w,
@@ -1201,9 +1232,14 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   SFM_REQUIRE(items < ((int64_t)1 << 31), "sweep too large for one launch");
   const int64_t blocks = (items + ipb - 1) / ipb;
   f32x4* tq = (f32x4*)ws;
+  Proj* projs = reinterpret_cast<Proj*>((char*)ws + sweep_quads_bytes(B, C, h, w));
+  float* depths = L <= kDepthTable ? reinterpret_cast<float*>((char*)projs + sweep_proj_bytes(B)) : nullptr;
   {
     ProfScope ps("sweep_tgt_quads", s);
-    launch_channel_quads(tgt, B, C, hw, tq, s);
+    const int64_t nq4 = (int64_t)B * g.C4 * hw;
+    const int64_t nthr = std::max(nq4, (int64_t)std::max(B, L));
+    hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, tgt, B, C, g.C4, hw, tq,
+                       pose, K4, K4inv, projs, L, g.dmax, g.dstep, depths);
   }
   SFM_LAUNCHED();
   const char* pname = with_ref ? "plane_sweep" : "plane_sweep_warped";
@@ -1277,15 +1313,16 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     fg.mhw = make_magic((unsigned)hw);
     fg.inv_w = 1.0f / (float)w;
     fg.dmax = g.dmax; fg.dstep = g.dstep;
+    fg.depths = depths;
     const unsigned blocks = (unsigned)((int64_t)B * fgroups * nwin);
     ProfScope ps(pname, s);
     if (mode == 2) {
       if (out_dtype == 0) {
-        if (nq == 2) launch_k_sweep_tile_nj<float, 2>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
-        else launch_k_sweep_tile_nj<float, 1>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+        if (nq == 2) launch_k_sweep_tile_nj<float, 2>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out, projs);
+        else launch_k_sweep_tile_nj<float, 1>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out, projs);
       } else {
-        if (nq == 2) launch_k_sweep_tile_nj<unsigned short, 2>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
-        else launch_k_sweep_tile_nj<unsigned short, 1>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
+        if (nq == 2) launch_k_sweep_tile_nj<unsigned short, 2>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out, projs);
+        else launch_k_sweep_tile_nj<unsigned short, 1>(nj, blocks, s, ref, tq, pose, K4, K4inv, fg, out, projs);
       }
     } else if (out_dtype == 0) launch_k_sweep_flat<float>(nq, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
     else launch_k_sweep_flat<unsigned short>(nq, blocks, s, ref, tq, pose, K4, K4inv, fg, out);
