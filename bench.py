@@ -96,8 +96,9 @@ def parse(argv=None):
 
 
 def _round_version(path):
-    """profiles/r02_pmc_v10.json -> (2, 10): numeric, so v10 sorts after v6."""
-    m = re.search(r"r(\d+)_pmc(?:_v(\d+))?\.json$", os.path.basename(path))
+    """profiles/r02_pmc_v10.json -> (2, 10): numeric, so v10 sorts after v6
+    (an optional config tag, r02_pmc_c3_v1.json, is allowed)."""
+    m = re.search(r"r(\d+)_pmc(?:_(?!v\d)[a-z0-9]+)?(?:_v(\d+))?\.json$", os.path.basename(path))
     return (int(m.group(1)), int(m.group(2) or 0)) if m else (-1, -1)
 
 

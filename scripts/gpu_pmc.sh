@@ -1,10 +1,11 @@
 #!/bin/bash
-# PMC counter passes over one short bench run (separate passes, kernel-trace only).
+# PMC counter passes over one short bench run (separate passes, kernel-trace only);
+# CONFIG selects the bench --config (c2 by default).
 set -u
 mkdir -p gpurun_out/pmc
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
-ARGS="python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-regularize"
+ARGS="python3 bench.py --config ${CONFIG:-c2} --steps 1 --warmup 1 --no-cpu-baseline --no-regularize"
 i=0
 for set in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" \

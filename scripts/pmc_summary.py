@@ -8,7 +8,7 @@ bytes of wide coalesced reads, so it is doubled; WRITE_SIZE is taken as is
 algorithmic byte count of the volume to 0.2%).  Infinity-Cache hits are
 counted in FETCH_SIZE, so re-reads of L3-resident inputs show up there.
 
-usage: python scripts/pmc_summary.py gpurun_out/pmc profiles/r02_pmc_v1.json
+usage: python scripts/pmc_summary.py gpurun_out/pmc profiles/r02_pmc_v1.json [config]
 """
 import collections
 import csv
@@ -34,7 +34,12 @@ def kernel_key(name):
     return None
 
 
-def main(src, dst):
+# bench.py CONFIGS: (pairs per GPU, scene, iters, nlabel, cost dtype, keypoints)
+WORKLOADS = {"c2": (8, 8, 128, "fp32"), "c3": (4, 8, 128, "bf16"), "c4": (8, 4, 64, "fp32"),
+             "sparse": (8, 8, 128, "fp32")}
+
+
+def main(src, dst, config="c2"):
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True)):
         acc = collections.defaultdict(float)
@@ -62,12 +67,14 @@ def main(src, dst):
         if "SQ_ACTIVE_INST_VALU" in m and "SQ_WAVE_CYCLES" in m:
             d["valu_active_frac_of_wave_cycles"] = round(m["SQ_ACTIVE_INST_VALU"] / m["SQ_WAVE_CYCLES"], 4)
         out[k] = d
+    b, it, nl, cd = WORKLOADS[config]
     json.dump({"source": "rocprofv3 --pmc --kernel-trace, separate passes (scripts/gpu_pmc.sh) over "
-                         "`python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline`",
+                         f"`python3 bench.py --config {config} --steps 1 --warmup 1 --no-cpu-baseline`",
+               "workload": {"config": config, "batch": b, "nlabel": nl, "iters": it, "cost_dtype": cd},
                "kernels": out}, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps({k: {x: v.get(x) for x in ("hbm_read_bytes", "hbm_write_bytes", "l2_hit_rate")}
                       for k, v in out.items()}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], *(sys.argv[3:4]))
