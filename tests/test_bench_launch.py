@@ -57,3 +57,25 @@ def test_pmc_summaries_sort_numerically():
     fs = ["profiles/r01_pmc_v6.json", "profiles/r01_pmc_v10.json", "profiles/r02_pmc.json", "profiles/r01_pmc.json"]
     assert sorted(fs, key=bench._round_version) == ["profiles/r01_pmc.json", "profiles/r01_pmc_v6.json",
                                                    "profiles/r01_pmc_v10.json", "profiles/r02_pmc.json"]
+    # a config tag is part of the name, not the version
+    assert bench._round_version("profiles/r02_pmc_c3_v1.json") == (2, 1)
+    assert bench._round_version("profiles/r01_conv_pmc.json") == (-1, -1)
+
+
+def test_pmc_traffic_matches_the_workload():
+    """The bench line's `traffic` comes only from a PMC summary collected on the
+    same workload: c2 and c3 each find their own file, a config without one
+    reports none."""
+    import types
+    sys.path.insert(0, ROOT)
+    import bench
+
+    def args(cfg):
+        b, _, it, nl, cd, _ = bench.CONFIGS[cfg]
+        return types.SimpleNamespace(config=cfg, batch=b, nlabel=nl, iters=it, cost_dtype=cd)
+
+    _, src2 = bench.pmc_traffic(args("c2"))
+    _, src3 = bench.pmc_traffic(args("c3"))
+    assert src2 and "_c3" not in src2
+    assert src3 and "_c3" in src3
+    assert bench.pmc_traffic(args("c4")) == ({}, None)
