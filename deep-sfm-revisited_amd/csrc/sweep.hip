@@ -1195,8 +1195,41 @@ static size_t sweep_quads_bytes(int B, int C, int h, int w) {
 // workspace: channel quads, then the per-pair Proj table
 constexpr int kDepthTable = 1024;   // plane depths kept in the workspace for L <= this
 static size_t sweep_proj_bytes(int B) { return ((size_t)B * sizeof(Proj) + 255) & ~(size_t)255; }
-static size_t sweep_ws_bytes(int B, int C, int h, int w) {
+// sfm_plane_sweep_psnet: float32 pose, K4, K4inv per pair (12 + 9 + 9 floats)
+static size_t sweep_psnet_bytes(int B) { return ((size_t)B * 30 * sizeof(float) + 255) & ~(size_t)255; }
+// what launch_sweep uses: quads, Proj table, plane depths
+static size_t sweep_core_bytes(int B, int C, int h, int w) {
   return sweep_quads_bytes(B, C, h, w) + sweep_proj_bytes(B) + kDepthTable * sizeof(float);
+}
+// the public size: the core plus the sfm_plane_sweep_psnet operands at its end
+static size_t sweep_ws_bytes(int B, int C, int h, int w) { return sweep_core_bytes(B, C, h, w) + sweep_psnet_bytes(B); }
+
+// The tensor preparation of PSNet.forward before its sweep loop, one thread per
+// pair, in the reference's float32 operations (PSNet.py:130-133 and the
+// RESCALE_DEPTH branch): P.float() (RNE from float64), translation * t_scale,
+// K rows 0-1 / 4, K^-1[:2,:2] * 4.  Division by 4 and multiplication by 4
+// are exact, and the conversion and the one multiply are correctly rounded,
+// so the results equal the torch ops bit for bit.
+__global__ void k_psnet_prep(int B, const void* __restrict__ pose, int pose_f64, const float* __restrict__ K,
+                             const float* __restrict__ Kinv, float t_scale, float* __restrict__ out) {
+  const int b = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (b >= B) return;
+  float* P = out + (size_t)b * 12;                       // planar: poses, then K4, then K4inv
+  float* K4 = out + (size_t)B * 12 + (size_t)b * 9;
+  float* Ki4 = out + (size_t)B * 21 + (size_t)b * 9;
+#pragma unroll
+  for (int e = 0; e < 12; ++e) {
+    float v = pose_f64 ? (float)static_cast<const double*>(pose)[(size_t)b * 12 + e]
+                       : static_cast<const float*>(pose)[(size_t)b * 12 + e];
+    if (t_scale > 0.0f && (e & 3) == 3) v = v * t_scale;
+    P[e] = v;
+  }
+#pragma unroll
+  for (int e = 0; e < 9; ++e) {
+    const float k = K[(size_t)b * 9 + e], ki = Kinv[(size_t)b * 9 + e];
+    K4[e] = e < 6 ? k / 4.0f : k;
+    Ki4[e] = (e == 0 || e == 1 || e == 3 || e == 4) ? ki * 4.0f : ki;
+  }
 }
 
 static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B, int C, int h, int w,
@@ -1208,7 +1241,7 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   SFM_REQUIRE(depth_mode == 0 || depth_mode == 1, "depth_mode must be 0 (inverse depth) or 1 (depth)");
   SFM_REQUIRE(min_depth > 0.0f, "min_depth must be positive");
   SFM_REQUIRE((int64_t)h * w < ((int64_t)1 << 30), "feature map too large");
-  const size_t need = sweep_ws_bytes(B, C, h, w);
+  const size_t need = sweep_core_bytes(B, C, h, w);
   if (!ws || ws_bytes < need) {
     set_error("plane sweep workspace too small: need " + std::to_string(need) + " bytes");
     return SFM_ERR_WORKSPACE;
@@ -1366,6 +1399,29 @@ int sfm_plane_sweep(const float* ref, const float* tgt, int batch, int channels,
   SFM_REQUIRE(ref, "null pointer argument");
   return launch_sweep(true, ref, tgt, batch, channels, h, w, pose, K4, K4inv, nlabel, min_depth, 0, out_dtype, cost,
                       workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int sfm_plane_sweep_psnet(const float* ref, const float* tgt, int batch, int channels, int h, int w,
+                          const void* pose, int pose_dtype, const float* K, const float* Kinv, float t_scale,
+                          int nlabel, float min_depth, int depth_mode, int out_dtype, void* cost, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  SFM_REQUIRE(tgt && pose && K && Kinv && cost && workspace, "null pointer argument");
+  SFM_REQUIRE(batch >= 1 && channels >= 1 && h >= 2 && w >= 2, "invalid sweep shape");
+  SFM_REQUIRE(pose_dtype == 0 || pose_dtype == 1, "pose_dtype must be 0 (float32) or 1 (float64)");
+  const size_t need = sweep_ws_bytes(batch, channels, h, w);
+  if (workspace_bytes < need) {
+    set_error("plane sweep workspace too small: need " + std::to_string(need) + " bytes");
+    return SFM_ERR_WORKSPACE;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  float* prep = reinterpret_cast<float*>((char*)workspace + sweep_core_bytes(batch, channels, h, w));
+  hipLaunchKernelGGL(k_psnet_prep, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, s, batch, pose, pose_dtype, K,
+                     Kinv, t_scale, prep);
+  SFM_LAUNCHED();
+  // the sweep's own scratch excludes the prep region at the workspace's end
+  return launch_sweep(ref != nullptr, ref, tgt, batch, channels, h, w, prep, prep + (size_t)batch * 12,
+                      prep + (size_t)batch * 21, nlabel, min_depth, depth_mode, out_dtype, cost, workspace,
+                      sweep_core_bytes(batch, channels, h, w), s);
 }
 
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w, const float* pose,

@@ -46,6 +46,10 @@ _SIGS = [
     ("sfm_plane_sweep_ex", ctypes.c_int,
      [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
       ctypes.c_float, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),
+    ("sfm_plane_sweep_psnet", ctypes.c_int,
+     [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, ctypes.c_int, _c_dp, _c_dp,
+      ctypes.c_float, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t,
+      _c_dp]),
     ("sfm_plane_sweep_warped", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, ctypes.c_int,
       ctypes.c_float, ctypes.c_int, _c_dp, _c_dp, ctypes.c_size_t, _c_dp]),

@@ -78,12 +78,10 @@ class TwoViewHotPath:
     def sweep(self, ref_fea, tgt_fea, P, K, Kinv=None):
         if Kinv is None:
             Kinv = self.k_inverse(K)
-        K4, Ki4 = sweep.quarter_intrinsics(K.float(), Kinv)
-        pose = P.float()
-        if self.rescale is not None:
-            pose[:, :, -1:] = pose[:, :, -1:] * self.rescale
-        return sweep.plane_sweep_cost(ref_fea, tgt_fea, pose, K4, Ki4, self.L, self.min_depth, self.cost_dtype,
-                                      out=self.cost, workspace=self.sweep_ws)
+        # PSNet.py:130-133 + RESCALE_DEPTH inside the sweep call (same float32 bits
+        # as quarter_intrinsics / P.float() * rescale, without ~10 ATen launches)
+        return sweep.plane_sweep_cost_psnet(ref_fea, tgt_fea, P, K, Kinv, self.L, self.min_depth, self.rescale,
+                                            self.cost_dtype, out=self.cost, workspace=self.sweep_ws)
 
     def step_pipelined(self, flow, K, ref_fea, tgt_fea):
         """``step`` with the sweep on a side stream: the pose stage runs on

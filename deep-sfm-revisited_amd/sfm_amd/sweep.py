@@ -84,6 +84,49 @@ def plane_sweep_cost(ref_fea, tgt_fea, pose, intrinsics4, intrinsics_inv4, nlabe
     return out
 
 
+def plane_sweep_cost_psnet(ref_fea, tgt_fea, pose, intrinsics, intrinsics_inv, nlabel, min_depth=1.0,
+                           rescale=None, dtype=torch.float32, out=None, workspace=None, predict_by_depth=False):
+    """``plane_sweep_cost`` from the pose stage's outputs: ``pose`` [B,3,4]
+    float32 or float64 (unscaled), full-resolution ``intrinsics`` /
+    ``intrinsics_inv`` [B,3,3].  PSNet.forward's preparation (P.float(),
+    RESCALE_DEPTH translation * ``rescale``, K/4 rows 0-1, K^-1[:2,:2]*4;
+    PSNet.py:130-133) runs inside the call (sfm_plane_sweep_psnet), with the
+    same float32 bits as ``quarter_intrinsics`` + ``plane_sweep_cost``.  Unlike
+    PlaneSweep it does not rescale the caller's pose in place."""
+    _refuse_grad(ref_fea=ref_fea, tgt_fea=tgt_fea, pose=pose, intrinsics=intrinsics, intrinsics_inv=intrinsics_inv)
+    tgt = _dev_f32(tgt_fea, "tgt_fea")
+    B, C, h, w = tgt.shape
+    ref = _dev_f32(ref_fea, "ref_fea")
+    if tuple(ref.shape) != (B, C, h, w):
+        raise RuntimeError(f"ref_fea shape {tuple(ref.shape)} != tgt_fea shape {(B, C, h, w)}")
+    if not pose.is_cuda:
+        raise RuntimeError("pose must be a CUDA tensor")
+    P = pose.reshape(B, 3, 4).contiguous()
+    if P.dtype not in (torch.float32, torch.float64):
+        P = P.float()
+    K = _dev_f32(intrinsics.reshape(B, 3, 3), "intrinsics")
+    Ki = _dev_f32(intrinsics_inv.reshape(B, 3, 3), "intrinsics_inv")
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise RuntimeError("cost dtype must be float32 or bfloat16")
+    shape = (B, 2 * C, int(nlabel), h, w)
+    if out is None:
+        out = torch.empty(shape, dtype=dtype, device=tgt.device)
+    elif tuple(out.shape) != shape or out.dtype != dtype or not out.is_contiguous() or out.device != tgt.device:
+        raise RuntimeError(f"out must be a contiguous {dtype} tensor of shape {shape} on {tgt.device}")
+    L = _lib.load()
+    if workspace is None:
+        workspace = workspace_for(B, C, h, w, tgt.device)
+    with torch.cuda.device(tgt.device):
+        rc = L.sfm_plane_sweep_psnet(_lib.ptr(ref), _lib.ptr(tgt), B, C, h, w, _lib.ptr(P),
+                                     1 if P.dtype == torch.float64 else 0, _lib.ptr(K), _lib.ptr(Ki),
+                                     float(rescale) if rescale is not None else 0.0, int(nlabel), float(min_depth),
+                                     1 if predict_by_depth else 0, 0 if dtype == torch.float32 else 1,
+                                     _lib.ptr(out), _lib.ptr(workspace), workspace.numel(),
+                                     _lib.stream_ptr(tgt.device))
+        _lib.check(rc, "sfm_plane_sweep_psnet")
+    return out
+
+
 def inverse_warp(feat, depth, pose, intrinsics, intrinsics_inv, padding_mode="zeros"):
     """models/inverse_warp.py:121-153 (bilinear, zeros padding, align_corners=True)."""
     check_sizes(depth, "depth", "BHW")

@@ -213,6 +213,20 @@ int sfm_plane_sweep_ex(const float* ref, const float* tgt, int batch, int channe
                        int nlabel, float min_depth, int depth_mode, int out_dtype, void* cost,
                        void* workspace, size_t workspace_bytes, void* stream);
 
+/* The sweep section of PSNet.forward from the pose stage's outputs, in one
+ * call (models/PSNet.py:130-157): the reference's tensor preparation runs in a
+ * one-thread-per-pair kernel instead of ~10 ATen launches, bit for bit:
+ *   pose      [dev] batch x 3 x 4, pose_dtype 0: float32, 1: float64 (P.float())
+ *   K, Kinv   [dev] batch x 3 x 3 float32, full resolution; K4 = K with rows
+ *             0-1 / 4, K4inv = Kinv with [:2,:2] * 4 (PSNet.py:130-133)
+ *   t_scale   > 0: translation column * t_scale in float32 (cfg.RESCALE_DEPTH);
+ *             <= 0: unscaled
+ * then as sfm_plane_sweep_ex (ref == NULL: warped half only). */
+int sfm_plane_sweep_psnet(const float* ref, const float* tgt, int batch, int channels, int h, int w,
+                          const void* pose, int pose_dtype, const float* K, const float* Kinv, float t_scale,
+                          int nlabel, float min_depth, int depth_mode, int out_dtype, void* cost,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
 /* Warped half only (cost[b, c, i] = inverse_warp(tgt, d_i)), batch x C x nlabel x h x w. */
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w,
                            const float* pose, const float* K4, const float* K4inv,

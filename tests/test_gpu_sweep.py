@@ -167,3 +167,34 @@ def test_full_size_kitti_bf16_volume(cuda):
     err = (got - want).abs() - (2.0 ** -8 * want.abs() + RTOL * torch.clamp(want.abs(), min=FLOOR))
     assert float(err.max()) <= 0.0, float((got - want).abs().max())
     assert float(want[:, C:].abs().sum()) > 0.0
+
+
+@pytest.mark.parametrize("pose_dtype,rescale,dtype,by_depth", [
+    (torch.float64, 0.6, torch.float32, False),     # the bench pipeline: RANSAC's float64 P, RESCALE_DEPTH
+    (torch.float32, None, torch.float32, True),
+    (torch.float64, 0.8, torch.bfloat16, False),
+])
+def test_psnet_entry_equals_torch_preparation(cuda, pose_dtype, rescale, dtype, by_depth):
+    """sfm_plane_sweep_psnet prepares pose / K4 / K4inv inside the call; the
+    volume must equal quarter_intrinsics + P.float() * rescale +
+    plane_sweep_cost bit for bit (PSNet.py:130-157)."""
+    from sfm_amd import synth
+    from sfm_amd.sweep import plane_sweep_cost, plane_sweep_cost_psnet, quarter_intrinsics
+    B, C, L = 3, 12, 9
+    h, w = 23, 70
+    ref, tgt = synth.features(B, C, h, w, seed=21)
+    K = synth.intrinsics(B, 4.0 * w, 4.1 * w, 2.0 * w, 2.0 * h).to(cuda)
+    Ki = torch.linalg.inv_ex(K)[0]
+    P = synth.relative_pose(B, torch.Generator().manual_seed(5)).to(pose_dtype).to(cuda)
+    P[:, :, 3] = P[:, :, 3] / P[:, :, 3].norm(dim=1, keepdim=True)
+    ref, tgt = ref.to(cuda), tgt.to(cuda)
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    pose = P.float()
+    if rescale is not None:
+        pose[:, :, -1:] = pose[:, :, -1:] * rescale
+    want = plane_sweep_cost(ref, tgt, pose, K4, Ki4, L, 0.9, dtype, predict_by_depth=by_depth)
+    P_before = P.clone()
+    got = plane_sweep_cost_psnet(ref, tgt, P, K, Ki, L, 0.9, rescale, dtype, predict_by_depth=by_depth)
+    assert torch.equal(got, want)
+    assert torch.equal(P, P_before)                 # the caller's pose is not rescaled in place
+    assert float(want[:, C:].float().abs().sum()) > 0.0
