@@ -1408,6 +1408,12 @@ int sfm_plane_sweep_psnet(const float* ref, const float* tgt, int batch, int cha
   SFM_REQUIRE(tgt && pose && K && Kinv && cost && workspace, "null pointer argument");
   SFM_REQUIRE(batch >= 1 && channels >= 1 && h >= 2 && w >= 2, "invalid sweep shape");
   SFM_REQUIRE(pose_dtype == 0 || pose_dtype == 1, "pose_dtype must be 0 (float32) or 1 (float64)");
+  // every argument launch_sweep checks, before the preparation kernel runs
+  SFM_REQUIRE(nlabel >= 1, "invalid sweep shape");
+  SFM_REQUIRE(out_dtype == 0 || out_dtype == 1, "out_dtype must be 0 (float32) or 1 (bfloat16)");
+  SFM_REQUIRE(depth_mode == 0 || depth_mode == 1, "depth_mode must be 0 (inverse depth) or 1 (depth)");
+  SFM_REQUIRE(min_depth > 0.0f, "min_depth must be positive");
+  SFM_REQUIRE((int64_t)h * w < ((int64_t)1 << 30), "feature map too large");
   const size_t need = sweep_ws_bytes(batch, channels, h, w);
   if (workspace_bytes < need) {
     set_error("plane sweep workspace too small: need " + std::to_string(need) + " bytes");

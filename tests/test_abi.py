@@ -109,6 +109,14 @@ def test_new_entry_points_validate_arguments():
     # plane sweep ex: bad depth mode, non-positive min depth
     assert lib.sfm_plane_sweep_ex(v, v, 1, 4, 8, 8, v, v, v, 4, 1.0, 2, 0, v, v, 1 << 20, None) == 1
     assert lib.sfm_plane_sweep_ex(v, v, 1, 4, 8, 8, v, v, v, 4, 0.0, 0, 0, v, v, 1 << 20, None) == 1
+    # plane sweep psnet: bad pose dtype, depth mode, min depth, null K, small workspace
+    ws = lib.sfm_plane_sweep_workspace_bytes(1, 4, 8, 8)
+    assert lib.sfm_plane_sweep_psnet(v, v, 1, 4, 8, 8, v, 2, v, v, 0.6, 4, 1.0, 0, 0, v, v, ws, None) == 1
+    assert lib.sfm_plane_sweep_psnet(v, v, 1, 4, 8, 8, v, 1, v, v, 0.6, 4, 1.0, 2, 0, v, v, ws, None) == 1
+    assert lib.sfm_plane_sweep_psnet(v, v, 1, 4, 8, 8, v, 1, v, v, 0.6, 4, 0.0, 0, 0, v, v, ws, None) == 1
+    assert lib.sfm_plane_sweep_psnet(v, v, 1, 4, 8, 8, v, 1, None, v, 0.6, 4, 1.0, 0, 0, v, v, ws, None) == 1
+    rc = lib.sfm_plane_sweep_psnet(v, v, 1, 4, 8, 8, v, 1, v, v, 0.6, 4, 1.0, 0, 0, v, v, ws - 1, None)
+    assert rc == 3 and b"workspace" in lib.sfm_last_error()
     # tuning knobs: unknown key / out of range
     assert lib.sfm_tune_set(b"no_such_knob", 1) == 1
     assert lib.sfm_tune_set(b"sweep_items_per_block", 3) == 1
