@@ -70,12 +70,15 @@ def test_pmc_traffic_matches_the_workload():
     sys.path.insert(0, ROOT)
     import bench
 
-    def args(cfg):
+    def args(cfg, batch=None):
         b, _, it, nl, cd, _ = bench.CONFIGS[cfg]
-        return types.SimpleNamespace(config=cfg, batch=b, nlabel=nl, iters=it, cost_dtype=cd)
+        return types.SimpleNamespace(config=cfg, batch=batch or b, nlabel=nl, iters=it, cost_dtype=cd)
 
     _, src2 = bench.pmc_traffic(args("c2"))
     _, src3 = bench.pmc_traffic(args("c3"))
-    assert src2 and "_c3" not in src2
+    _, src4 = bench.pmc_traffic(args("c4"))
+    assert src2 and "_c3" not in src2 and "_c4" not in src2
     assert src3 and "_c3" in src3
-    assert bench.pmc_traffic(args("c4")) == ({}, None)
+    assert src4 and "_c4" in src4
+    # same config, a batch no summary was collected on
+    assert bench.pmc_traffic(args("c2", batch=3)) == ({}, None)
