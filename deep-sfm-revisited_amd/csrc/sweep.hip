@@ -332,6 +332,7 @@ struct FlatGeom {
   int out_mis;     // element offset of the output pointer modulo amask + 1
   int pair_ok;     // bf16: every row starts at an even element (4-byte pair stores)
   int buf_ok;      // k_sweep_tile fast path: per-pair volume, ref and quad ranges < 2^32 bytes, pair_ok
+  int share;       // k_sweep_tile fast path: neighbour-lane tap sharing (tuning key sweep_share)
   unsigned pair_bytes;   // one pair's output volume in bytes (buffer range)
   Magic mwin, mgrp, mhw;
   float inv_w;
@@ -713,7 +714,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uns
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
 
-template <typename OutT, int NQ, int NJ>
+// Lane i + 1's value in lane i (DPP wave_shl:1; lane 63 reads 0).
+__device__ __forceinline__ unsigned next_lane_u(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xf, 0xf, true);
+}
+__device__ __forceinline__ float next_lane_f(float v) { return __uint_as_float(next_lane_u(__float_as_uint(v))); }
+
+template <typename OutT, int NQ, int NJ, bool SHARE>
 __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, const f32x4* __restrict__ tq,
                                                 const Proj* __restrict__ projs, const FlatGeom& g,
                                                 OutT* __restrict__ out, int b, int k, int start) {
@@ -778,7 +785,55 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
     float ix, iy;
 #pragma unroll
     for (int n = 0; n < NQ; ++n) acc[n][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (sample_pos_nr(pr, ray, d, sk, ix, iy)) {
+    if (SHARE) {
+      // Lanes hold consecutive pixels, and a fronto-parallel plane maps
+      // neighbouring pixels ~one source pixel apart: lane i's right-hand taps
+      // (off[1], off[3]) are usually lane i + 1's left-hand taps (off[0],
+      // off[2]).  Each lane gathers its left-hand taps, takes the right-hand
+      // ones from the next lane where the offsets are equal (then the values
+      // are the same memory words), and gathers them itself elsewhere: half
+      // the tap gathers through the texture path, the same bits.
+      const bool in = sample_pos_nr(pr, ray, d, sk, ix, iy);
+      TapsIn tp;
+      if (in) {
+        make_taps_inside(ix, iy, g.h, g.w, tp);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { tp.off[e] = 0u; tp.wt[e] = 0.0f; }
+      }
+      const unsigned n0 = next_lane_u(tp.off[0]), n2 = next_lane_u(tp.off[2]);
+      const unsigned nin = next_lane_u(in ? 1u : 0u);
+      const bool own = in && !(nin != 0u && n0 == tp.off[1] && n2 == tp.off[3]);
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        const unsigned so = (unsigned)n * g.hw * 16u;
+        f32x4 t[4];
+        t[0] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        t[2] = t[0];
+        if (in) {
+          t[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtq, tp.off[0] * 16u, so, 0));
+          t[2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtq, tp.off[2] * 16u, so, 0));
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          t[1][e] = next_lane_f(t[0][e]);
+          t[3][e] = next_lane_f(t[2][e]);
+        }
+        if (own) {
+          t[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtq, tp.off[1] * 16u, so, 0));
+          t[3] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtq, tp.off[3] * 16u, so, 0));
+        }
+        f32x4 a;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = tp.wt[0] * t[0][e];
+          v = __builtin_fmaf(tp.wt[1], t[1][e], v);
+          v = __builtin_fmaf(tp.wt[2], t[2][e], v);
+          a[e] = __builtin_fmaf(tp.wt[3], t[3][e], v);
+        }
+        if (in) acc[n][j] = a;
+      }
+    } else if (sample_pos_nr(pr, ray, d, sk, ix, iy)) {
       TapsIn tp;
       make_taps_inside(ix, iy, g.h, g.w, tp);
 #pragma unroll
@@ -847,7 +902,10 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
   const int start = win * WIN - (int)((wbase + (size_t)g.out_mis) & (size_t)g.amask);
   if (start >= g.slab) return;
   if (g.buf_ok && start >= 0 && start + WIN <= g.slab && (k + 1) * 4 * NQ <= g.C)
-    sweep_tile_fast<OutT, NQ, NJ>(ref, tq, projs, g, out, b, k, start);
+  {
+    if (g.share) sweep_tile_fast<OutT, NQ, NJ, true>(ref, tq, projs, g, out, b, k, start);
+    else sweep_tile_fast<OutT, NQ, NJ, false>(ref, tq, projs, g, out, b, k, start);
+  }
   else if (start >= 0 && start + WIN <= g.slab)
     sweep_tile_item<OutT, NQ, NJ, true>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
   else
@@ -1340,6 +1398,7 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     fg.pair_ok = (slab % 2 == 0) && ((uintptr_t)out % 4 == 0);
     const int64_t pair_bytes = (int64_t)g.rows * slab * esz;
     fg.buf_ok = pair_bytes < ((int64_t)1 << 32) && (out_dtype == 0 || fg.pair_ok) && tuning().sweep_buffer;
+    fg.share = tuning().sweep_share;
     fg.pair_bytes = fg.buf_ok ? (unsigned)pair_bytes : 0u;
     fg.mwin = make_magic((unsigned)nwin);
     fg.mgrp = make_magic((unsigned)fgroups);

@@ -303,6 +303,8 @@ int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int chann
  *     "sweep_items_per_block" 1,2,4,8 work items per block of the per-row sweep (4)
  *     "sweep_nj"              1,2,4   pixels per lane of k_sweep_tile (1; bf16 uses 2)
  *     "sweep_buffer"          0, 1    buffer-addressed interior path of k_sweep_tile (1)
+ *     "sweep_share"           0, 1    k_sweep_tile interior path: right-hand bilinear taps
+ *                                     from the next lane where the offsets match (0)
  *     "sweep_run"             1..1024 planes per block of k_sweep_band (16)
  *     "sweep_band_rows"       2..64   target rows k_sweep_band stages in LDS (16,
  *                                     clipped to 80 KB per block)

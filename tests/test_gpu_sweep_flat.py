@@ -120,3 +120,36 @@ def test_band_kernel_full_size_kitti(cuda, dtype, run, rows):
         _lib.tune("sweep_band_rows", 16)
     assert torch.equal(got, want)
     assert float(want[:, C:].float().abs().sum()) > 0.0
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,L,hw,tscale,by_depth", [
+    (2, 32, 128, None, 0.6, False),     # the bench's volume (94x311, RESCALE_DEPTH pose)
+    (1, 32, 64, None, 3.0, True),       # large baseline, depth planes: taps far apart
+    (2, 16, 8, (40, 300), 0.6, False),  # windows across row and plane ends
+    (1, 8, 5, (13, 64), 1.0, False),    # hw < 256: windows span several planes
+])
+def test_shared_taps_equal_gathered(cuda, dtype, B, C, L, hw, tscale, by_depth):
+    """sweep_share=1 (k_sweep_tile's interior path takes each lane's right-hand
+    taps from the next lane where the tap offsets are equal) writes the same
+    bits as the gathering path, whatever the share rate."""
+    from sfm_amd import _lib, synth
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
+    h, w = hw or synth.feature_hw()
+    ref, tgt = synth.features(B, C, h, w, seed=C + L)
+    K = synth.intrinsics(B, 4.0 * w, 4.0 * w, 2.0 * w, 2.0 * h) if hw else synth.intrinsics(B)
+    Ki = torch.inverse(K)
+    pose = synth.relative_pose(B, torch.Generator().manual_seed(L))
+    pose[:, :, 3] *= tscale / pose[:, :, 3].norm(dim=1, keepdim=True)
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    args = (ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 1.0)
+    old = _lib.tune_get("sweep_share")
+    try:
+        outs = []
+        for share in (0, 1):
+            _lib.tune("sweep_share", share)
+            outs.append(plane_sweep_cost(*args, dtype=dtype, predict_by_depth=by_depth))
+    finally:
+        _lib.tune("sweep_share", old)
+    assert torch.equal(outs[0], outs[1])
+    assert float(outs[0][:, C:].float().abs().sum()) > 0.0
