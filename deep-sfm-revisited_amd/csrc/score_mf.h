@@ -57,8 +57,17 @@ typedef float mf_float16 __attribute__((ext_vector_type(16)));
 #define SFM_MF_SUB 3
 #endif
 constexpr int kMfSub = SFM_MF_SUB;            // candidate groups per item (one staged span serves them all)
-constexpr int kMfWaves = 12;                // waves per block (3 per SIMD): one 32-candidate tile each
-constexpr int kMfSpan = 768;                // points per item (B fragments staged in LDS)
+#ifndef SFM_MF_WAVES
+#define SFM_MF_WAVES 12
+#endif
+#ifndef SFM_MF_SPAN
+#define SFM_MF_SPAN 768
+#endif
+#ifndef SFM_MF_WPE
+#define SFM_MF_WPE (SFM_MF_WAVES / 4)
+#endif
+constexpr int kMfWaves = SFM_MF_WAVES;      // waves per block (3 per SIMD): one 32-candidate tile each
+constexpr int kMfSpan = SFM_MF_SPAN;        // points per item (B fragments staged in LDS)
 constexpr int kMfTiles = kMfSpan / 32;
 constexpr int kMfQueue = 256;               // undecided entries per wave (drained in windows of this size)
 constexpr int kMfRec = 64;                  // f16 per candidate: 4 A rows of K = 16
@@ -443,7 +452,7 @@ __device__ __forceinline__ void lds_barrier() {
 
 
 template <class Src, bool SAME>
-__global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(kMfWaves / 4, kMfWaves / 4))) void k_score_mf(const Src src, PairParams pp, int batch, int cmax,
+__global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(SFM_MF_WPE, SFM_MF_WPE))) void k_score_mf(const Src src, PairParams pp, int batch, int cmax,
                                                            const int32_t* __restrict__ cand_total,
                                                            const double* __restrict__ candE,
                                                            const _Float16* __restrict__ candF,
