@@ -333,6 +333,7 @@ struct FlatGeom {
   int pair_ok;     // bf16: every row starts at an even element (4-byte pair stores)
   int buf_ok;      // k_sweep_tile fast path: per-pair volume, ref and quad ranges < 2^32 bytes, pair_ok
   int share;       // k_sweep_tile fast path: neighbour-lane tap sharing (tuning key sweep_share)
+  int store_nt;    // k_sweep_tile fast path: non-temporal volume stores (tuning key sweep_store_nt)
   unsigned pair_bytes;   // one pair's output volume in bytes (buffer range)
   Magic mwin, mgrp, mhw;
   float inv_w;
@@ -720,7 +721,7 @@ __device__ __forceinline__ unsigned next_lane_u(unsigned v) {
 }
 __device__ __forceinline__ float next_lane_f(float v) { return __uint_as_float(next_lane_u(__float_as_uint(v))); }
 
-template <typename OutT, int NQ, int NJ, bool SHARE>
+template <typename OutT, int NQ, int NJ, bool SHARE, bool NT>
 __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, const f32x4* __restrict__ tq,
                                                 const Proj* __restrict__ projs, const FlatGeom& g,
                                                 OutT* __restrict__ out, int b, int k, int start) {
@@ -856,19 +857,27 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
     }
   }
   const bool odd = (lane & 1) != 0;
+  // volume stores: with NT the cache policy is sc0 nt (non-temporal, the
+  // volume is never re-read by this kernel), so the 7.7 GB of streaming
+  // writes do not evict the reference rows and target quads that every plane
+  // re-reads from L2 (tuning key sweep_store_nt, profiles/r02_sweep_nt_ab.txt:
+  // bf16 0.474 -> 0.442 ms; fp32 1.255 -> 1.265, so by default bf16 only)
+  auto bstore = [&](unsigned v, __amdgpu_buffer_rsrc_t r, unsigned off, unsigned so) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off, so, NT ? 3 : 0);
+  };
   // row r of the pair: soffset r * row_bytes; per-lane byte offset(s) of the window
   auto store_row = [&](unsigned r, const float* v) {
     const unsigned so = r * row_bytes;
     if (!BF) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), rout, (unsigned)(woff + 64 * j + lane) * 4u, so, 0);
+        bstore(__float_as_uint(v[j]), rout, (unsigned)(woff + 64 * j + lane) * 4u, so);
     } else {
 #pragma unroll
       for (int s = 0; s < NJ / 2; ++s) {
         const unsigned u = bf16_pair_swap(to_bf16(v[2 * s]), to_bf16(v[2 * s + 1]), odd);
         const int f = woff + 128 * s + lane + (odd ? 63 : 0);
-        __builtin_amdgcn_raw_buffer_store_b32(u, rout, (unsigned)f * 2u, so, 0);
+        bstore(u, rout, (unsigned)f * 2u, so);
       }
     }
   };
@@ -903,8 +912,13 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
   if (start >= g.slab) return;
   if (g.buf_ok && start >= 0 && start + WIN <= g.slab && (k + 1) * 4 * NQ <= g.C)
   {
-    if (g.share) sweep_tile_fast<OutT, NQ, NJ, true>(ref, tq, projs, g, out, b, k, start);
-    else sweep_tile_fast<OutT, NQ, NJ, false>(ref, tq, projs, g, out, b, k, start);
+    if (g.store_nt) {
+      if (g.share) sweep_tile_fast<OutT, NQ, NJ, true, true>(ref, tq, projs, g, out, b, k, start);
+      else sweep_tile_fast<OutT, NQ, NJ, false, true>(ref, tq, projs, g, out, b, k, start);
+    } else {
+      if (g.share) sweep_tile_fast<OutT, NQ, NJ, true, false>(ref, tq, projs, g, out, b, k, start);
+      else sweep_tile_fast<OutT, NQ, NJ, false, false>(ref, tq, projs, g, out, b, k, start);
+    }
   }
   else if (start >= 0 && start + WIN <= g.slab)
     sweep_tile_item<OutT, NQ, NJ, true>(ref, tq, pose, K4, K4inv, g, out, b, k, start, wbase);
@@ -1399,6 +1413,7 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     const int64_t pair_bytes = (int64_t)g.rows * slab * esz;
     fg.buf_ok = pair_bytes < ((int64_t)1 << 32) && (out_dtype == 0 || fg.pair_ok) && tuning().sweep_buffer;
     fg.share = tuning().sweep_share;
+    fg.store_nt = tuning().sweep_store_nt == 2 ? out_dtype != 0 : tuning().sweep_store_nt;   // auto: bf16 only
     fg.pair_bytes = fg.buf_ok ? (unsigned)pair_bytes : 0u;
     fg.mwin = make_magic((unsigned)nwin);
     fg.mgrp = make_magic((unsigned)fgroups);

@@ -305,6 +305,9 @@ int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int chann
  *     "sweep_buffer"          0, 1    buffer-addressed interior path of k_sweep_tile (1)
  *     "sweep_share"           0, 1    k_sweep_tile interior path: right-hand bilinear taps
  *                                     from the next lane where the offsets match (0)
+ *     "sweep_store_nt"        0,1,2   k_sweep_tile's volume stores non-temporal (sc0 nt)
+ *                                     so they do not evict the re-read operands
+ *                                     (2: bf16 volumes only)
  *     "sweep_run"             1..1024 planes per block of k_sweep_band (16)
  *     "sweep_band_rows"       2..64   target rows k_sweep_band stages in LDS (16,
  *                                     clipped to 80 KB per block)

@@ -1,7 +1,8 @@
 """Same-process A/B of sweep tuning keys on the bench volume (KITTI B pairs,
 L=128, 94x311, C=32): per-launch plane_sweep time from the library's HIP-event
 profiler, 10 launches per variant and round, three interleaved rounds; every
-variant's volume must equal the first variant's bit for bit.
+variant's volume must equal the first variant's bit for bit.  AB_ROUNDS
+rounds (default 3), odd rounds in reverse variant order.
 Usage: sweep_ab.py [dtype=bf16] [B=4] "k=v,k=v" "k=v" ..."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -11,6 +12,7 @@ from sfm_amd import _lib, synth
 from sfm_amd import sweep as SW
 
 dtype, B, names = torch.float32, 8, []
+ROUNDS = int(os.environ.get("AB_ROUNDS", "3"))
 for a in sys.argv[1:]:
     if a.startswith("dtype="):
         dtype = torch.bfloat16 if a.split("=")[1] == "bf16" else torch.float32
@@ -31,8 +33,9 @@ ws = SW.workspace_for(B, C, h, w, dev)
 nbytes = out.numel() * out.element_size() + ref.numel() * 4 + tgt.numel() * 4
 res = {i: [] for i in range(len(variants))}
 base = None
-for rnd in range(3):
-    for i, v in enumerate(variants):
+for rnd in range(ROUNDS):
+    order = list(enumerate(variants))
+    for i, v in (order if rnd % 2 == 0 else order[::-1]):
         for k, x in v.items():
             _lib.tune(k, int(x))
         out.fill_(float("nan"))

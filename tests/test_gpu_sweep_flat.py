@@ -132,7 +132,9 @@ def test_band_kernel_full_size_kitti(cuda, dtype, run, rows):
 def test_shared_taps_equal_gathered(cuda, dtype, B, C, L, hw, tscale, by_depth):
     """sweep_share=1 (k_sweep_tile's interior path takes each lane's right-hand
     taps from the next lane where the tap offsets are equal) writes the same
-    bits as the gathering path, whatever the share rate."""
+    bits as the gathering path, whatever the share rate; so do the
+    non-temporal volume stores (sweep_store_nt; by default bf16 only) and
+    plain ones."""
     from sfm_amd import _lib, synth
     from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
     h, w = hw or synth.feature_hw()
@@ -143,13 +145,16 @@ def test_shared_taps_equal_gathered(cuda, dtype, B, C, L, hw, tscale, by_depth):
     pose[:, :, 3] *= tscale / pose[:, :, 3].norm(dim=1, keepdim=True)
     K4, Ki4 = quarter_intrinsics(K, Ki)
     args = (ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 1.0)
-    old = _lib.tune_get("sweep_share")
+    old = _lib.tune_get("sweep_share"), _lib.tune_get("sweep_store_nt")
     try:
         outs = []
-        for share in (0, 1):
+        for share, nt in ((0, 0), (1, 0), (0, 1), (1, 1)):
             _lib.tune("sweep_share", share)
+            _lib.tune("sweep_store_nt", nt)
             outs.append(plane_sweep_cost(*args, dtype=dtype, predict_by_depth=by_depth))
     finally:
-        _lib.tune("sweep_share", old)
-    assert torch.equal(outs[0], outs[1])
+        _lib.tune("sweep_share", old[0])
+        _lib.tune("sweep_store_nt", old[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
     assert float(outs[0][:, C:].float().abs().sum()) > 0.0
