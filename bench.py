@@ -271,12 +271,12 @@ def _main_stub(args, dist):
     if rank == 0:
         print(json.dumps({"metric": "stub", "value": world * args.batch * args.steps / elapsed, "unit": "pairs/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "dist": {"world_size": torch.distributed.get_world_size() if world > 1 else 1,
-                                   "backend": torch.distributed.get_backend() if world > 1 else None,
+                          "dist": {"world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
+                                   "backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
                                    "devices": names},
                           "config": {"name": args.config, "pairs_per_gpu": args.batch,
                                      "global_batch": world * args.batch}}), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
     return 0
 
@@ -369,8 +369,8 @@ def _main_gpu(args, dist):
                        "pairs_per_gpu": B, "global_batch": world * B, "parallelism": f"dp{world}",
                        "streams": "sweep on a side stream (overlaps the next step's solve)" if args.pipeline
                        else "one stream"},
-            "dist": {"world_size": torch.distributed.get_world_size() if world > 1 else 1,
-                     "backend": torch.distributed.get_backend() if world > 1 else None,
+            "dist": {"world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
+                     "backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
                      "devices": names},
             "roofline": score_roofline(use_mf, score_tflops, done, evals, skipped, sum(cands), hp.n, score_ms,
                                        traffic.get("ransac_score"), traffic_src),
@@ -396,7 +396,7 @@ def _main_gpu(args, dist):
             except Exception as e:   # the baseline is reported, never the target
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
     return 0
 

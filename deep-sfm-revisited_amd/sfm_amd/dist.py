@@ -17,9 +17,12 @@ def env_rank():
 
 
 def init(backend=None):
-    """Initialise the default process group from torchrun's environment (no-op for world 1)."""
+    """Initialise the default process group from torchrun's environment.  A
+    plain single process (no WORLD_SIZE / MASTER_PORT) stays without one; a
+    torchrun world of 1 gets one, so the RCCL path runs on a one-GPU box too."""
     rank, world, local = env_rank()
-    if world > 1 and not dist.is_initialized():
+    launched = "WORLD_SIZE" in os.environ and "MASTER_PORT" in os.environ
+    if (world > 1 or launched) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"

@@ -86,3 +86,25 @@ def test_two_rank_gloo_matches_single_process(tmp_path, num_pairs):
     assert np.all(got[:, -1] == 2.0)                                 # max over ranks
     want = np.stack([_solve_pair(i) for i in range(num_pairs)])
     assert np.array_equal(got[:, 1:-1], want)                        # bit-identical per pair
+
+
+def test_torchrun_world_of_one_gets_a_process_group():
+    """Under torchrun (WORLD_SIZE and MASTER_PORT set) a world of 1 initialises
+    the process group, so a one-GPU box runs the RCCL barrier / max-reduce
+    path; a plain process (no torchrun variables) stays without one."""
+    import subprocess
+    code = ("import sys; sys.path.insert(0, {pkg!r}); import torch.distributed as d; "
+            "from sfm_amd import dist; r = dist.init('gloo'); "
+            "print(d.is_initialized(), r, dist.reduce_max(2.5))").format(
+                pkg=os.path.join(ROOT, "deep-sfm-revisited_amd"))
+    base = {k: v for k, v in os.environ.items()
+            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    launched = dict(base, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                    MASTER_PORT=str(_free_port()))
+    out = subprocess.run([sys.executable, "-c", code], env=launched, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    last = out.stdout.strip().splitlines()[-1]          # gloo may log a line first
+    assert last.split()[0] == "True" and last.endswith("2.5")
+    out = subprocess.run([sys.executable, "-c", code], env=base, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1].split()[0] == "False"
