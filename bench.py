@@ -78,8 +78,10 @@ def parse(argv=None):
                     help="skip the (unscored) PSNet 3-D regularisation roofline line after the timed region")
     ap.add_argument("--fused", action="store_true",
                     help="RANSAC reads the flow directly (sfm_ransac5_flow) instead of materialised correspondences")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-runs", type=int, default=3, help="full-pair CPU baseline runs (median)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for the CPU baseline: 16 = the host-core share one GPU gets on the "
+                         "MI355X pool (nproc there reports the whole 256-thread host)")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="full-pair CPU baseline runs (median; BASELINE.md: >= 5)")
     ap.add_argument("--pipeline", action="store_true",
                     help="each step's sweep on a side stream, overlapping the next step's pose stage "
                          "(TwoViewHotPath.step_pipelined): c2 +1.7 %%, sparse +12 %% pairs/s, but the overlapped "
@@ -140,6 +142,14 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
             "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work}
 
 
+def metric_name(nlabel, hwtxt):
+    """BASELINE.json's metric for its own workload (KITTI, nlabel=128); the
+    same form with this run's plane count and image shape otherwise."""
+    if nlabel == 128 and hwtxt.startswith("KITTI"):
+        return "image-pairs/sec (5-pt RANSAC + nlabel=128 plane-sweep), KITTI 376\u00d71242"
+    return f"image-pairs/sec (5-pt RANSAC + nlabel={nlabel} plane-sweep), {hwtxt}"
+
+
 def cpu_info(threads):
     import torch
     model = "unknown"
@@ -191,8 +201,11 @@ def cpu_baseline(flow, K, ref_fea, tgt_fea, pose, args, n_pts=None, keypoints=No
     out = {"value": round(1.0 / per_pair, 4), "unit": "pairs/s", "kind": "port",
            "sample": (f"1 full pair, median of {len(tr)} runs after a warm-up: RANSAC 512 chains x {args.iters} "
                       f"iters on N={q.shape[0]} ({t_ransac:.2f} s, oracle C++ OpenMP), {args.nlabel}-plane sweep "
-                      f"({t_sweep:.3f} s, torch-CPU fp32)")}
+                      f"({t_sweep:.3f} s, torch-CPU fp32)"),
+           "runs_s": [round(a + b, 3) for a, b in zip(tr, ts)]}
     out.update(cpu_info(threads))
+    out["threads_reason"] = ("the host-core share of one GPU on this pool (16); nproc/affinity show the whole "
+                             "host" if threads == 16 else "--cpu-threads")
     return out
 
 
@@ -268,9 +281,13 @@ def _main_stub(args, dist):
     dist.barrier()
     elapsed = dist.reduce_max(time.perf_counter() - t0)
     names = dist.device_names(None)
+    # the same per-pair gather as the GPU path: rows tagged (rank, pair)
+    rows = torch.tensor([[float(rank), float(i)] for i in range(args.batch)], dtype=torch.float64)
+    gathered = dist.gather_rows(rows, world)
     if rank == 0:
         print(json.dumps({"metric": "stub", "value": world * args.batch * args.steps / elapsed, "unit": "pairs/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "gathered": {"pairs": int(gathered.shape[0]), "rows": gathered.tolist()},
                           "dist": {"world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
                                    "backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
                                    "devices": names},
@@ -325,6 +342,10 @@ def _main_gpu(args, dist):
     _lib.profile_enable(False)
     elapsed = dist.reduce_max(elapsed, dev)
     names = dist.device_names(dev)
+    # validation outputs of every rank's pairs to rank 0 (replaces
+    # DataParallel's output gather, main.py:219): E[9], P[12], inliers per pair
+    rows = torch.cat([E.reshape(B, 9), P.reshape(B, 12), inl.reshape(B, 1).double()], 1)
+    gathered = dist.gather_rows(rows, world).cpu()
 
     kt = {}
     for name in ("flow_to_points", "keypoints_to_points", "ransac_solve", "ransac_chain", "ransac_score",
@@ -351,7 +372,7 @@ def _main_gpu(args, dist):
         pairs = world * B * args.steps
         corr = (f"{args.keypoints} SIFT-like keypoints" if args.keypoints else f"dense flow (N={hp.n})")
         out = {
-            "metric": "image-pairs/sec (5-pt RANSAC + nlabel=128 plane-sweep), KITTI 376x1242",
+            "metric": metric_name(args.nlabel, hwtxt),
             "value": round(pairs / elapsed, 3),
             "unit": "pairs/s",
             "n_gpus": world,
@@ -362,7 +383,8 @@ def _main_gpu(args, dist):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64+" + ("f32" if s == 4 else "bf16"),
-            "data": "synthetic (seeded KITTI-shaped rigid scene, 0.5 px noise, 15% outlier flow; N(0,1) features)",
+            "data": (f"synthetic (seeded {hwtxt.split()[0]}-shaped rigid scene, 0.5 px noise, 15% outlier flow, "
+                     f"{corr}; N(0,1) features)"),
             "config": {"name": args.config,
                        "workload": (f"{hwtxt} {corr}, H={512 * args.iters} hypotheses (ransac_iter={args.iters}), "
                                     f"nlabel={args.nlabel}, C=32 at {h}x{w}, {args.cost_dtype} cost volume"),
@@ -382,7 +404,10 @@ def _main_gpu(args, dist):
             "solve": {"hypotheses_per_launch": hyps, "ms": round(kt["ransac_solve"], 4),
                       "hypotheses_per_s": round(hyps / (kt["ransac_solve"] * 1e-3), 1)},
             "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
-            "inliers": [int(v) for v in inl.cpu()],
+            "inliers": [int(v) for v in gathered[:, 21].tolist()],
+            "gathered": {"pairs": int(gathered.shape[0]), "per_rank": [len(dist.shard(world * B, r, world))
+                                                                       for r in range(world)],
+                         "via": "dist.gather_rows (all_gather of E[9], P[12], inliers per pair)"},
         }
         if world == 1 and not args.no_regularize and hp.cost.dtype in (torch.float32, torch.bfloat16):
             try:

@@ -59,6 +59,7 @@ struct Workspace {
   double* hypP0;       // [B][H][12]
   double* sstate;      // [kStateFields][B][H]: solve state between k_solve_front, k_roots, k_solve_back
   int32_t* cand_off;   // [B][H]
+  int32_t* chain_ref;  // [B][H] (latest k <= i with a root) + 1 | (latest k < i with a candidate) + 1 << 16
   int32_t* cand_total; // [64]
   double* candE;       // [B][Cmax][12]
   int32_t* cntT;       // [B][Cmax]
@@ -86,6 +87,7 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   t.hypP0 = (double*)take(bc * H * 12 * 8);
   t.sstate = (double*)take((size_t)kStateFields * bc * H * 8);
   t.cand_off = (int32_t*)take(bc * H * 4);
+  t.chain_ref = (int32_t*)take(bc * H * 4);
   t.cand_total = (int32_t*)take(SFM_MAX_BATCH * 4);
   t.candE = (double*)take(bc * C * kCandStride * 8);
   t.cntT = (int32_t*)take(bc * C * 4);
@@ -416,8 +418,9 @@ __device__ __forceinline__ void fp32_constants(const double* E, double thr, bool
 //            over chains (chain t owns hypotheses t*iters .. t*iters+iters-1)
 //   k_cand   one thread per (hypothesis, slot): the candidate records
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kChains) void k_chain(int H, int iters, const int32_t* __restrict__ ncand,
-                                                   int32_t* __restrict__ cand_off, int32_t* __restrict__ cand_total) {
+__global__ __launch_bounds__(kChains) void k_chain(int H, int iters, const int32_t* __restrict__ nroots,
+                                                   const int32_t* __restrict__ ncand, int32_t* __restrict__ cand_off,
+                                                   int32_t* __restrict__ chain_ref, int32_t* __restrict__ cand_total) {
   __shared__ int32_t s_sum[kChains / 64];
   const int b = blockIdx.x, t = threadIdx.x;
   const size_t hb0 = (size_t)b * H + (size_t)t * iters;
@@ -438,18 +441,26 @@ __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, const int32
   int off = incl - cnt;
   for (int w = 0; w < wv; ++w) off += s_sum[w];
   if (t == kChains - 1) cand_total[b] = off + cnt;
+  // the same walk records, per hypothesis, the slot-0 state the reference
+  // thread holds (kernel_functions.cu:154, 179): the chain's latest hypothesis
+  // with a root (E) up to i, and with an accepted candidate (P) before i, so
+  // that k_cand reads them in O(1) instead of looking back along the chain
+  int ke = -1, kp = -1;
   for (int i = 0; i < iters; ++i) {
     const int nc = ncand[hb0 + i];
+    if (nroots[hb0 + i] > 0) ke = i;
     cand_off[hb0 + i] = off;
+    chain_ref[hb0 + i] = (ke + 1) | ((kp + 1) << 16);
     off += nc > 0 ? nc : 1;
+    if (nc > 0) kp = i;
   }
 }
 
 // A hypothesis with no candidate rescores slot 0 as the reference thread
 // holds it (kernel_functions.cu:154, 179-214): E of the chain's latest
 // hypothesis with a root, P of its latest with an accepted candidate (zeros
-// before any).  The thread finds them by looking back along its chain.
-__global__ __launch_bounds__(256) void k_cand(int H, int iters, int cheir, const int32_t* __restrict__ nroots,
+// before any), as k_chain recorded them (chain_ref).
+__global__ __launch_bounds__(256) void k_cand(int H, int iters, int cheir, const int32_t* __restrict__ chain_ref,
                                               const int32_t* __restrict__ ncand, const double* __restrict__ hypE,
                                               const double* __restrict__ hypP, double* __restrict__ hypP0,
                                               const int32_t* __restrict__ cand_off, double* __restrict__ candE,
@@ -470,12 +481,8 @@ __global__ __launch_bounds__(256) void k_cand(int H, int iters, int cheir, const
   } else {
     const int i = h % iters;
     const size_t c0 = hb - i;   // the chain's first hypothesis
-    int ke = -1, kp = -1;
-    for (int k = i; k >= 0 && ke < 0; --k)
-      if (nroots[c0 + k] > 0) ke = k;
-    if (cheir)
-      for (int k = i - 1; k >= 0 && kp < 0; --k)
-        if (ncand[c0 + k] > 0) kp = k;
+    const int ref = chain_ref[hb];
+    const int ke = (ref & 0xffff) - 1, kp = cheir ? (ref >> 16) - 1 : -1;
 #pragma unroll
     for (int e = 0; e < 9; ++e) dst[e] = ke >= 0 ? hypE[(c0 + ke) * kMaxSlots * 9 + e] : 0.0;
 #pragma unroll
@@ -922,7 +929,7 @@ __device__ __forceinline__ int score32_pass(const double* __restrict__ CE, int c
     // enqueue after the unrolled compares (enqueueing inside them splits the
     // FMA block per point and costs SGPRs)
 #pragma unroll
-    for (int k = 0; k < kPPL32; ++k) enqueue_undecided(undk[k], c, pl + 64 * k, lane, q, qn);
+    for (int k = 0; k < kPPL32; ++k) enqueue_undecided(undk[k], c, pl + 64 * k, lane, q, qn);   // pl: relative to the item
     if (SAME || !MASKED) sR = sT;
     if (lane == 0) {
       cnt[c][0] += sT;
@@ -937,8 +944,8 @@ __device__ __forceinline__ int score32_pass(const double* __restrict__ CE, int c
 constexpr int kDrainBatch = 4;
 
 template <class Src>
-__device__ __forceinline__ void score32_drain(const double* __restrict__ CE, const Src& src, int b, int T, int R,
-                                              const ScoreConsts& kc, int lane, int32_t (*cnt)[2],
+__device__ __forceinline__ void score32_drain(const double* __restrict__ CE, const Src& src, int b, int p0, int T,
+                                              int R, const ScoreConsts& kc, int lane, int32_t (*cnt)[2],
                                               const uint32_t* q, int qn) {
 #pragma unroll 1
   for (int i0 = 0; i0 < qn; i0 += 64 * kDrainBatch) {
@@ -948,12 +955,12 @@ __device__ __forceinline__ void score32_drain(const double* __restrict__ CE, con
     for (int j = 0; j < kDrainBatch; ++j) {
       const int i = i0 + 64 * j + lane;
       e[j] = i < qn ? q[i] : 0xffffffffu;
-      v[j] = src.load(b, e[j] != 0xffffffffu ? (int)(e[j] & 0xffffffu) : 0);
+      v[j] = src.load(b, p0 + (e[j] != 0xffffffffu ? (int)(e[j] & 0xffffffu) : 0));
     }
 #pragma unroll
     for (int j = 0; j < kDrainBatch; ++j) {
       if (e[j] == 0xffffffffu) continue;
-      const int c = (int)(e[j] >> 24), p = (int)(e[j] & 0xffffffu);
+      const int c = (int)(e[j] >> 24), p = p0 + (int)(e[j] & 0xffffffu);
       if (inlier_f64v(CE + (size_t)c * kCandStride, v[j], kc)) {
         if (p < T) atomicAdd(&cnt[c][0], 1);
         if (p < R) atomicAdd(&cnt[c][1], 1);
@@ -1080,18 +1087,18 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
         const float M2 = Mf * Mf;
         const int nT = min(p1, T) - cb, nR = min(p1, R) - cb;
         if (min(nT, nR) >= 64 * kPPL32) {                           // no prefix masking needed
-          if (unit) c = score32_pass<true, false, false>(CE, c, nc, pl, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
-          else c = score32_pass<true, false, true>(CE, c, nc, pl, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
+          if (unit) c = score32_pass<true, false, false>(CE, c, nc, pl - p0, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
+          else c = score32_pass<true, false, true>(CE, c, nc, pl - p0, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
         } else if (T == R) {
-          c = score32_pass<true, true, true>(CE, c, nc, pl, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
+          c = score32_pass<true, true, true>(CE, c, nc, pl - p0, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
         } else {
-          c = score32_pass<false, true, true>(CE, c, nc, pl, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
+          c = score32_pass<false, true, true>(CE, c, nc, pl - p0, nT, nR, x, y, xp, yp, M2, bad, kc, lane, cnt, queue, qn);
         }
         c = __builtin_amdgcn_readfirstlane(c);
         if (c >= nc) break;
 #ifndef SFM_SCORE_NOFALLBACK
         wave_sync();                                      // queue past its low mark: drain, resume at c
-        score32_drain(CE, src, b, T, R, kc, lane, cnt, queue, qn);
+        score32_drain(CE, src, b, p0, T, R, kc, lane, cnt, queue, qn);
         qn = 0;
         wave_sync();
 #endif
@@ -1099,7 +1106,7 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
     }
 #ifndef SFM_SCORE_NOFALLBACK
     wave_sync();
-    score32_drain(CE, src, b, T, R, kc, lane, cnt, queue, qn);
+    score32_drain(CE, src, b, p0, T, R, kc, lane, cnt, queue, qn);
 #endif
     wave_sync();
     if (kc.prune) {
@@ -1305,7 +1312,7 @@ void k_score_mx(const Src src, PairParams pp, int batch, int cmax, const int32_t
       for (int cb = p0; cb < p1; cb += 32) {
         if (qn > kQueueMX - 1024) {                      // drain before a block could overflow the queue
           wave_sync();
-          score32_drain(CE, src, b, T, R, kc, lane, cnt, queue, qn);
+          score32_drain(CE, src, b, p0, T, R, kc, lane, cnt, queue, qn);
           qn = 0;
           wave_sync();
         }
@@ -1347,14 +1354,14 @@ void k_score_mx(const Src src, PairParams pp, int batch, int cmax, const int32_t
             if ((und >> lane) & 1ull) {
               const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(und >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)und, 0));
-              queue[pos] = ((uint32_t)mx_row(r, half) << 24) | (uint32_t)p;
+              queue[pos] = ((uint32_t)mx_row(r, half) << 24) | (uint32_t)(p - p0);   // relative to the item
             }
             qn += __popcll(und);
           }
         }
       }
       wave_sync();
-      score32_drain(CE, src, b, T, R, kc, lane, cnt, queue, qn);
+      score32_drain(CE, src, b, p0, T, R, kc, lane, cnt, queue, qn);
       wave_sync();
       // per-row totals: sum over the 32 lanes of each half
 #pragma unroll
@@ -1620,8 +1627,9 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   const bool fast32 = fast && thr >= 0x1p-20 && tuning().score_fp32;
   {
     ProfScope ps("ransac_chain", s);
-    hipLaunchKernelGGL(k_chain, dim3(bc), dim3(kChains), 0, s, H, iters, w.ncand, w.cand_off, w.cand_total);
-    hipLaunchKernelGGL(k_cand, dim3((H * kMaxSlots + 255) / 256, bc), dim3(256), 0, s, H, iters, cheir, w.nroots,
+    hipLaunchKernelGGL(k_chain, dim3(bc), dim3(kChains), 0, s, H, iters, w.nroots, w.ncand, w.cand_off, w.chain_ref,
+                       w.cand_total);
+    hipLaunchKernelGGL(k_cand, dim3((H * kMaxSlots + 255) / 256, bc), dim3(256), 0, s, H, iters, cheir, w.chain_ref,
                        w.ncand, w.hypE, w.hypP, w.hypP0, w.cand_off, w.candE, cmax, guard_g, thr, fast32 ? 1 : 0);
   }
   SFM_LAUNCHED();

@@ -315,8 +315,8 @@ __device__ __forceinline__ void mf_drain(const double* __restrict__ sE, const do
 #pragma unroll 1
   for (int i = lane; i < qn; i += 64) {
     const uint32_t e = q[i];
-    const int c = (int)(e >> 24), p = (int)(e & 0xffffffu);
-    if (inlier_f64v(sE + c * 10, spts[p - p0], kc)) {
+    const int c = (int)(e >> 24), r = (int)(e & 0xffffffu), p = p0 + r;   // r: index in the span
+    if (inlier_f64v(sE + c * 10, spts[r], kc)) {
       if (p < T) atomicAdd(&cnt[c][0], 1);
       if (p < R) atomicAdd(&cnt[c][1], 1);
     }
@@ -663,13 +663,14 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(S
         int pos = incl - nl - base;
         if (qtotal <= kMfQueue) {
           // the usual case, one window: every entry fits, no bounds test.
-          // Entry = row << 24 | point; bit j of a string is tile ntiles-1-j,
-          // point p0 + 32 (ntiles-1-j) + rl = top - 32 j.
+          // Entry = row << 24 | span-relative point (< kMfSpan, so any N fits);
+          // bit j of a string is tile ntiles-1-j, point 32 (ntiles-1-j) + rl
+          // of the span = top - 32 j.
           uint32_t* q = queue + pos;
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
             uint32_t u = ~(s1[g] | s2[g]) & vm;
-            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(p0 + 32 * (ntiles - 1) + rl);
+            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (ntiles - 1) + rl);
             while (u) {
               *q++ = top - 32u * (uint32_t)__builtin_ctz(u);
               u &= u - 1u;
@@ -679,7 +680,7 @@ __global__ __launch_bounds__(kMfWaves * 64) __attribute__((amdgpu_waves_per_eu(S
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
             uint32_t u = ~(s1[g] | s2[g]) & vm;
-            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(p0 + 32 * (ntiles - 1) + rl);
+            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (ntiles - 1) + rl);
             while (u) {
               if (pos >= 0 && pos < kMfQueue) queue[pos] = top - 32u * (uint32_t)__builtin_ctz(u);
               u &= u - 1u;

@@ -11,10 +11,17 @@ branch (``pose_by_ransac``) runs on libsfm_hip for the whole batch at once:
   RANSAC            one batched sfm_ransac5_packed launch over all pairs
                     (the reference loops over pairs, SFMnet.py:216-272)
 
-Out of scope (tier framing) and therefore injected: the flow
-estimator (RAFT / DICL), the depth estimator (PSNet & co.; see
-sfm_amd.depth.CorrelationDepth for a parameter-free one built on the hot
-path), the keypoint matcher (cv2 SIFT/SURF + FLANN, absent here) and PoseNet.
+Default construction follows SFMnet.__init__ (SFMnet.py:33-75): with
+cfg.DEPTH_EST == 'PSNET' (the default) ``SFMnet(nlabel)`` builds
+``sfm_amd.psnet.PSNet(nlabel, min_depth)`` -- PSNet's module layout with the
+sweep, the 3-D regularisation and the head on libsfm_hip -- so
+``SFMnet(args.nlabel)`` (main.py:198) runs as it stands.  Out of scope
+(tier framing) and therefore injected: the flow estimator (RAFT /
+DICL: ``flow_estimator=``; its absence is a named RuntimeError when forward
+needs a flow), the other depth estimators (CVP, PANet, REGNet, REG2D,
+DISPNET: a named RuntimeError at construction unless ``depth_estimator=`` is
+given), the keypoint matcher (cv2 SIFT/SURF + FLANN, absent here) and
+PoseNet.
 """
 import time
 
@@ -29,7 +36,7 @@ time_dict = {}
 
 class SFMnet(torch.nn.Module):
     def __init__(self, nlabel=64, min_depth=0.5, flow_estimator=None, depth_estimator=None, matcher=None,
-                 cfg=None):
+                 cfg=None, feature_fn=None):
         super().__init__()
         self.cfg = _default_cfg if cfg is None else cfg
         c = self.cfg
@@ -43,6 +50,13 @@ class SFMnet(torch.nn.Module):
         self.nlabel = nlabel
         self.min_depth = min_depth
         self.flow_estimator = flow_estimator
+        if depth_estimator is None:
+            kind = c.get("DEPTH_EST", "PSNET")
+            if kind != "PSNET":
+                raise RuntimeError(f"SFMnet: cfg.DEPTH_EST={kind!r} is not built here (only PSNET, SFMnet.py:57-58); "
+                                   f"pass depth_estimator= (a module with PSNet.forward's signature)")
+            from sfm_amd.psnet import PSNet
+            depth_estimator = PSNet(nlabel, min_depth, cfg=c, feature_fn=feature_fn)
         self.depth_estimator = depth_estimator
         # matcher(ref_img_hwc_uint8, tgt_img_hwc_uint8) -> (pts1 [n,2], pts2 [n,2]) or None;
         # stands in for SIFT/SURF detectAndCompute + FLANN ratio test (SFMnet.py:190-214)
@@ -55,7 +69,7 @@ class SFMnet(torch.nn.Module):
                 h_side=None, w_side=None, logger=None, depth_gt=None, img_path=None):
         c = self.cfg
         if self.training and c.get("TRAIN_FLOW", False):
-            return self.flow_estimator(torch.cat((ref, target), dim=1))
+            return self._flow()(torch.cat((ref, target), dim=1))
 
         intrinsic_gpu = intrinsic.float().cuda()
         intrinsic_inv_gpu = torch.inverse(intrinsic_gpu)
@@ -64,7 +78,7 @@ class SFMnet(torch.nn.Module):
             if c.PRED_POSE_ONLINE:
                 flow_start = time.time()
                 with torch.autocast("cuda", enabled=bool(c.MIXED_PREC)):
-                    flow_2D, conf = self.flow_estimator(torch.cat((ref, target), dim=1))
+                    flow_2D, conf = self._flow()(torch.cat((ref, target), dim=1))
                 time_dict["flow"] = time.time() - flow_start
                 if h_side is not None or w_side is not None:
                     flow_2D = flow_2D[:, :, :h_side, :w_side]
@@ -109,6 +123,14 @@ class SFMnet(torch.nn.Module):
         if self.training:
             return flow_2D, P_mat, depth, depth_init, rot_and_trans
         return flow_2D, P_mat, depth, time_dict
+
+    def _flow(self):
+        if self.flow_estimator is None:
+            raise RuntimeError(f"SFMnet: this forward needs optical flow, and cfg.FLOW_EST="
+                               f"{self.cfg.get('FLOW_EST', 'DICL')!r} (RAFT / DICL) is out of scope here: pass "
+                               f"flow_estimator= (images [B,6,H,W] -> (flow [B,2,H,W], conf)), or use GT / "
+                               f"predicted poses")
+        return self.flow_estimator
 
     # ------------------------------------------------------------------
     def _matches(self, ref, target, h_side, w_side):

@@ -35,13 +35,20 @@ def defaults():
         RECORD_POSE=False,        # lib/config.py:147
         RECORD_POSE_EVAL=False,   # lib/config.py:149
         PREDICT_BY_DEPTH=False,   # lib/config.py:91
+        TRAIN_FLOW=False,         # lib/config.py
+        FLOW_EST="DICL",          # lib/config.py:178 (RAFT / DICL: out of scope, injected)
+        DEPTH_EST="PSNET",        # lib/config.py:181 (PSNET built by default; others injected)
+        PSNET_CONTEXT=True,       # lib/config.py:46
+        PSNET_DEP_CONTEXT=False,  # lib/config.py:47
+        IND_CONTEXT=False,        # lib/config.py:164
+        CONTEXT_BN=False,         # lib/config.py:158
     )
 
 
 def kitti():
     c = defaults()
     c.update(MIXED_PREC=True, RESCALE_DEPTH=True, NORM_TARGET=0.6, MIN_DEPTH=1.0, ransac_iter=5,
-             PRED_POSE_ONLINE=True)   # cfgs/kitti.yml:10-41
+             PRED_POSE_ONLINE=True, PSNET_DEP_CONTEXT=True)   # cfgs/kitti.yml:10-41
     return c
 
 

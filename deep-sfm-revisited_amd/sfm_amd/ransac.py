@@ -86,19 +86,28 @@ class score_precision:
     calls inside it (tuning key "score_precision", process-wide): 64 (the
     default) reproduces the reference's float64 decisions exactly; 32 / 16
     evaluate ComputeError<float> / <half> (approximate inlier sets; BASELINE
-    C5's fp32-vs-fp16 sweep).  Not thread-safe across concurrent callers."""
+    C5's fp32-vs-fp16 sweep).  Nests: leaving restores the precision that was
+    in force on entry.  Not thread-safe across concurrent callers.
+
+    The 32 / 16 arithmetic is this build's variant of the reference's template
+    (kernel_functions.cu:231-264), which is only ever instantiated with
+    T = double there: here E, the products and the sums are all held in T
+    (see DESIGN.md "Reduced-precision scoring"); its parity is unpinned by any
+    reference output."""
 
     def __init__(self, bits):
         if int(bits) not in (64, 32, 16):
             raise ValueError("score precision must be 64, 32 or 16")
         self.bits = int(bits)
+        self._saved = []
 
     def __enter__(self):
+        self._saved.append(int(_lib.tune_get("score_precision")))
         _lib.tune("score_precision", self.bits)
         return self
 
     def __exit__(self, *exc):
-        _lib.tune("score_precision", 64)
+        _lib.tune("score_precision", self._saved.pop())
 
 
 def ransac5_batched(pts, n=None, num_test_points=None, num_ransac_test_points=None, iters=5, threshold=1e-4,

@@ -139,8 +139,11 @@ class CostRegularization(nn.Module):
         self._packed, self._packed_key = packed, key
         return packed
 
-    def forward(self, cost):
-        """cost [B, Cin, L, h, w] fp32 or bf16 (the sweep's volume) -> [B, 1, L, h, w] fp32."""
+    def forward(self, cost, precision="bf16"):
+        """cost [B, Cin, L, h, w] fp32 or bf16 (the sweep's volume) -> [B, 1, L, h, w] fp32.
+        ``precision``: "bf16" (bf16 activations and weights, fp32 accumulation)."""
+        if precision != "bf16":
+            raise ValueError(f"unknown conv precision {precision!r}")
         if not (isinstance(cost, torch.Tensor) and cost.is_cuda):
             raise RuntimeError("CostRegularization.forward needs a device tensor (HIP path, no CPU fallback)")
         if cost.dtype not in (torch.float32, torch.bfloat16) or cost.dim() != 5:

@@ -27,6 +27,48 @@ def _build_oracle():
     yield
 
 
+@pytest.hookimpl(trylast=True)
+def pytest_collection_modifyitems(session, config, items):
+    """The two-rank GPU test (test_gpu_dist.py) needs its ranks started as
+    fresh processes before this process touches the GPU: start them here,
+    after collection and deselection, before any test runs.
+    torch.cuda.device_count() does not initialise the GPU."""
+    if not any("test_gpu_dist.py" in it.nodeid for it in items):
+        return
+    import tempfile
+    import torch
+    if torch.cuda.device_count() < 1:
+        return
+    out = tempfile.mkdtemp(prefix="sfm_dist_")
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SFM_DIST_OUT=out)
+        log = open(os.path.join(out, f"rank{r}.log"), "w")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "helpers", "dist_gpu_worker.py")],
+                                      env=env, stdout=log, stderr=subprocess.STDOUT))
+    config._sfm_dist_ranks = (procs, out)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="session")
+def dist_gpu_ranks(request):
+    ranks = getattr(request.config, "_sfm_dist_ranks", None)
+    if ranks is None:
+        pytest.skip("ranks not started (no GPU, or the test was not collected at session start)")
+    yield ranks
+    for p in ranks[0]:
+        if p.poll() is None:
+            p.kill()
+
+
 def load_golden(name):
     """npz -> nested dict ("group/key" entries become d[group][key])."""
     z = np.load(os.path.join(GOLDEN, name), allow_pickle=False)

@@ -34,6 +34,9 @@ def test_spawns_two_ranks_without_torchrun():
     assert out["dist"]["world_size"] == 2 and out["dist"]["backend"] == "gloo"
     assert out["dist"]["devices"] == ["cpu", "cpu"]
     assert out["config"]["pairs_per_gpu"] == 4 and out["config"]["global_batch"] == 8
+    # every rank's pairs reach rank 0, in rank order
+    assert out["gathered"]["pairs"] == 8
+    assert out["gathered"]["rows"] == [[float(r), float(i)] for r in range(2) for i in range(4)]
 
 
 def test_single_rank_default():
