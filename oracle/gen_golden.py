@@ -443,6 +443,18 @@ def gen_psnet():
     return out
 
 
+def gen_psnet_keys():
+    """state_dict key -> shape of the reference PSNet as SFMnet builds it by
+    default (SFMnet.py:57-58) with cfgs/kitti.yml's PSNET_DEP_CONTEXT: pins
+    sfm_amd.psnet.PSNet's module layout (a reference checkpoint loads)."""
+    with _RefEnv() as env:
+        cfg = env.import_("lib.config").cfg
+        cfg.update(PSNET_CONTEXT=True, PSNET_DEP_CONTEXT=True, IND_CONTEXT=False)
+        PS = env.import_("models.PSNet")
+        net = PS.PSNet(128, 1.0)
+        return {k: list(v.shape) for k, v in net.state_dict().items()}
+
+
 def _save(name, d):
     flat = {}
     for k, v in d.items():
@@ -460,7 +472,7 @@ def main(argv=None):
     """python -m oracle.gen_golden [name ...]  (default: every fixture)."""
     import sys
     want = set((sys.argv[1:] if argv is None else argv) or
-               ["solve5", "ransac", "irls", "sampler", "warp", "corr", "psnet"])
+               ["solve5", "ransac", "irls", "sampler", "warp", "corr", "psnet", "psnet_keys"])
     os.makedirs(OUT, exist_ok=True)
     rng = np.random.default_rng(20241015)
     # the rng is consumed in this order, so a subset regenerates identical files
@@ -477,6 +489,12 @@ def main(argv=None):
         _save("corr.npz", gen_corr())
     if "psnet" in want:
         _save("psnet.npz", gen_psnet())
+    if "psnet_keys" in want:
+        import json
+        path = os.path.join(OUT, "psnet_keys.json")
+        with open(path, "w") as f:
+            json.dump(gen_psnet_keys(), f, indent=0, sort_keys=True)
+        print("wrote", path)
 
 
 if __name__ == "__main__":

@@ -169,3 +169,56 @@ def test_end_to_end_with_sweep_depth(cuda):
     want = S.depth_head(cost, 32, 1.0, HW)
     rel = ((depth.cpu() - want).abs() / want.abs()).max()
     assert float(rel) <= 1e-4, float(rel)
+
+
+def _psnet_inputs(cuda, B=1, H=128, W=192):
+    from sfm_amd import synth
+    g = torch.Generator().manual_seed(3)
+    ref = (torch.rand(B, 3, H, W, generator=g) * 2 - 1).to(cuda)
+    tgt = (torch.rand(B, 3, H, W, generator=g) * 2 - 1).to(cuda)
+    K = synth.intrinsics(B, 100.0, 98.0, 95.5, 63.5).to(cuda)
+    a = torch.tensor([[0, -0.02, 0.01], [0.02, 0, -0.015], [-0.01, 0.015, 0.0]])
+    pose = torch.cat([torch.matrix_exp(a), torch.tensor([[0.2], [-0.05], [-1.2]])], 1)
+    return ref, tgt, K, pose.reshape(1, 3, 4).repeat(B, 1, 1).to(cuda)
+
+
+def test_default_sfmnet_runs_as_main_builds_it(cuda):
+    """SFMnet(nlabel) with no injected estimators (main.py:198): GT pose, the
+    PSNet-layout depth estimator (feature CNN, HIP sweep + regularisation +
+    head, context networks), eval return tuple; a predicted pose without a
+    flow estimator is a named error."""
+    from models.SFMnet import SFMnet
+    from sfm_amd.config import kitti
+    c = kitti()
+    c.update(MIXED_PREC=False)
+    torch.manual_seed(0)
+    m = SFMnet(16, 1.0, cfg=c).to(cuda).eval()
+    ref, tgt, K, pose = _psnet_inputs(cuda)
+    with torch.no_grad():
+        flow, P_mat, depth, _ = m(ref, tgt, K, pose_gt=pose, use_gt_pose=True)
+    assert P_mat.shape == (1, 1, 3, 4) and flow.shape == (1, 2, 128, 192)
+    assert depth.shape == (1, 1, 128, 192) and bool(torch.isfinite(depth).all())
+    with pytest.raises(RuntimeError, match="flow_estimator="):
+        m(ref, tgt, K, pose_gt=pose)
+
+
+def test_psnet_without_context_is_the_hot_path_chain(cuda):
+    """PSNet with PSNET_CONTEXT off: both outputs equal psnet_depth (sweep ->
+    CostRegularization -> head) on the module's own features, bit for bit."""
+    from sfm_amd.config import defaults
+    from sfm_amd.psnet import PSNet
+    from sfm_amd.regularize import psnet_depth
+    c = defaults()
+    c.update(PSNET_CONTEXT=False, RESCALE_DEPTH=True, NORM_TARGET=0.6)
+    torch.manual_seed(1)
+    net = PSNet(16, 1.0, cfg=c).to(cuda).eval()
+    ref, tgt, K, pose = _psnet_inputs(cuda)
+    Kinv = torch.inverse(K)
+    P = pose.unsqueeze(1).clone()
+    with torch.no_grad():
+        d_init, d = net(ref, [tgt], P, K, Kinv)
+        assert torch.allclose(P[:, 0, :, 3], pose[:, :, 3] * 0.6)           # RESCALE_DEPTH in place
+        want = psnet_depth(net.feature_extraction(ref).float(), net.feature_extraction(tgt).float(), P[:, 0],
+                           K, Kinv, net.regularize, 16, 1.0, out_hw=(128, 192))
+    assert torch.equal(d_init, d)
+    assert torch.equal(d, want)
