@@ -110,7 +110,7 @@ const TuneKey kTuneKeys[] = {
     {"score_fp32", &sfm::Tuning::score_fp32, v_01},
     {"score_prune", &sfm::Tuning::score_prune, v_01},
     {"score_mfma", &sfm::Tuning::score_mfma, v_01},
-    {"score_mf", &sfm::Tuning::score_mf, v_01},
+    {"score_mf", &sfm::Tuning::score_mf, [](int v) { return v >= 0 && v <= 2; }},
     {"score_mf_blocks_per_cu", &sfm::Tuning::score_mf_blocks_per_cu, [](int v) { return v >= 1 && v <= 8; }},
     {"score_interleave", &sfm::Tuning::score_interleave, v_01},
     {"conv_rolling", &sfm::Tuning::conv_rolling, v_01},

@@ -1590,6 +1590,7 @@ __global__ void k_keypoint_points(const float* __restrict__ flow, int H, int W, 
 // Host launchers
 // ---------------------------------------------------------------------------
 #include "score_mf.h"
+#include "score_mf2.h"
 
 template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
@@ -1665,7 +1666,10 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
       hipLaunchKernelGGL(k_mf_cands, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax, w.cand_total, w.candE,
                          w.candF, mp);
       const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
-      if (same)
+      if (same && tuning().score_mf == 2)
+        hipLaunchKernelGGL(k_score_mf2<Src>, dim3(std::max(1, cus)), dim3(kMf2Waves * 64), 0, s, src, pp, bc, cmax,
+                           w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
+      else if (same)
         hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
                            w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
       else

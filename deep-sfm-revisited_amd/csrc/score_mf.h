@@ -28,20 +28,32 @@
 //     when c_lo is subnormal), same for m; the dropped c_lo m_lo <= 2^-22 |c m|
 //     -> 3 * 2^-22 S + 18 * 2^-25 (max|c| + M^2); the monomials are formed in
 //     float32 from float32 coordinates, +0.75 * 2^-22 S (3.75 * 2^-22 in all).
-//   * MFMA accumulation: measured on gfx950 (scripts/probe_mfma_f16.hip, 4.1M
-//     elements incl. adversarial magnitudes): |D - exact| <= 7.95 u (|C| +
-//     sum|ab|); the bound used is 16 u (|C| + sum|ab|) per MFMA: 16u S (1 +
-//     2^-9) for the hi x hi MFMA, 16u (|a| + 2^-8 S) for the second.
+//   * MFMA accumulation (derived, whatever the rounding): each f16 x f16
+//     product is exact in f32 (11 x 11 significand bits, exponents in range),
+//     so a v_mfma_f32_32x32x16_f16 output is the sum of n = 17 exact operands
+//     (16 products and C).  If every one of its n - 1 additions rounds
+//     faithfully in f32 (to nearest, toward zero or any direction: error < 1
+//     ulp = 2u of the partial sum, whose magnitude is <= sum|operands|), in any
+//     order or tree, the error is <= (n - 1) 2u sum|ops| = 32u (|C| + sum|ab|).
+//     If instead the adder aligns all n operands to the largest exponent and
+//     truncates each at 24 bits before one final rounding, the error is <=
+//     n 2u max|op| + 2u |result| <= 36u (|C| + sum|ab|).  The bound used is
+//     K_acc = SFM_MF_ACC_U u with SFM_MF_ACC_U = 36 (the larger; the
+//     round-2 build used 16, above the 7.95u measured by
+//     scripts/probe_mfma_f16.hip but not derived): K_acc S (1 + 2^-9) for the
+//     hi x hi MFMA, K_acc (|a| + 2^-8 S) for the second.
 //   * the reference's own float64 rounding: 2^-46 S absolute, 2^-40 relative.
-//   => |a'_computed - a'| <= alpha = aS * |c|_1 M^2 + ... + 16u |a'|; the
-//      16u |a'| part is a relative factor folded into t (1 -/+ 2^-18).
+//   => |a'_computed - a'| <= alpha = aS * |c|_1 M^2 + ... + K_acc |a'|; the
+//      K_acc |a'| part (<= 36u < 2^-18) is a relative factor folded into t
+//      (1 -/+ 2^-18).
 //   * certain inlier: (|a| + alpha)^2 <= (1 + 2^-6) a^2 + 65 alpha^2 (AM-GM)
 //     <= t D  <=  aa < t_lo D - eps1,  t_lo = t / (1 + 2^-6) (and the
 //     aa rounding 2^-22, ...), eps1 = 65 alpha^2 / (1 + 2^-6).
 //     certain outlier: aa > t_hi D + eps2, t_hi = t / (1 - 2^-6), eps2 = 64
 //     alpha^2 / (1 - 2^-6) (if |a| < alpha the test cannot fire).
 //   * Ylo / Yhi themselves: f16 coefficients and monomials (2^-11 relative
-//     each) and the accumulation: eta <= 1.048e-3 (>= 2^-10 + 2^-20 + margin) sum|g_j| M^2 (+ subnormal
+//     each) and the accumulation: eta <= 1.048e-3 (>= 2^-10 + K_acc + margin,
+//     K_acc = 36u = 2^-18.8) sum|g_j| M^2 (+ subnormal
 //     terms), subtracted from / added to the coefficients of M^2; eps via M^4.
 //     Directed rounding keeps every eps / eta coefficient >= its bound.
 // Validity: 2^-15 <= thr < 1 (k in [0, 15]), finite non-zero E (zero E scores
@@ -49,6 +61,11 @@
 // evaluation goes to float64), M <= 15.9 per point (else float64).
 // Numerically emulated before the kernel was written: 0 wrong decisions and
 // 0.65 % undecided over 28M evaluations of 1398 KITTI candidates.
+
+#ifndef SFM_MF_ACC_U
+#define SFM_MF_ACC_U 36
+#endif
+static_assert(SFM_MF_ACC_U <= 64, "the relative part K_acc |a'| must stay below the 2^-18 folded into t");
 
 typedef _Float16 mf_half8 __attribute__((ext_vector_type(8)));
 typedef float mf_float16 __attribute__((ext_vector_type(16)));
@@ -181,7 +198,8 @@ __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, con
     //   K3 = aS |c_8| + 2^-24 + 9 * 2^-24 max|c|,  C1 / C2 = max |c| over each group;
     //   alpha^2 <= 3 (K1^2 s1^2 + K2^2 s2^2 + K3^2)   (Cauchy-Schwarz)
     // eps terms ride on the monomials (s1/4)^2, (s2/4)^2 and '1'.
-    const double aS = 16.0 * 0x1p-24 * (1.0 + 0x1p-9) + 3.75 * 0x1p-22 + 16.0 * 0x1p-24 * 0x1p-8 + 0x1p-46;
+    constexpr double kAcc = SFM_MF_ACC_U * 0x1p-24;          // MFMA accumulation bound per operand sum
+    const double aS = kAcc * (1.0 + 0x1p-9) + 3.75 * 0x1p-22 + kAcc * 0x1p-8 + 0x1p-46;
     const double C1 = fmax(fmax(fabs(cc[0]), fabs(cc[1])), fmax(fabs(cc[3]), fabs(cc[4])));
     const double C2 = fmax(fmax(fabs(cc[2]), fabs(cc[5])), fmax(fabs(cc[6]), fabs(cc[7])));
     const double K1 = aS * C1 + 0x1p-24, K2 = aS * C2 + 0x1p-24;

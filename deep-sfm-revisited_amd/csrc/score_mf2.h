@@ -1,0 +1,273 @@
+// Phase 3e of the RANSAC (included by ransac5.hip after score_mf.h): the
+// span-major split-f16 matrix-core scorer, k_score_mf2 (default for SFMnet's
+// num_test == num_ransac_test; tuning key score_mf = 2).
+//
+// Same arithmetic and decisions as k_score_mf (the A rows of k_mf_cands, the
+// B columns of mf_stage_point, mf_tile_mfma, mf_tile_decide, the float64
+// re-test of the undecided band), so every count is identical; what changes
+// is how the work is laid out on the chip:
+//
+//   * Work units are (pair, 1024-point span, 32-candidate tile), ordered
+//     span-major within a pair, and each persistent block takes one
+//     contiguous range of ~U / grid units.  The block stages a span once
+//     (B fragments + float64 points, one LDS image) and its 12 waves run
+//     every candidate tile of that span in its range, 25-26 each per span at
+//     KITTI size; one LDS barrier pair per span, not per candidate group.
+//     The per-pair tail of k_score_mf (the last candidate group of a pair
+//     leaving up to half the waves of an item idle) does not exist: the
+//     range split is exact to one unit.
+//   * Logical block ranges are contiguous per XCD (block id % 8 picks the
+//     XCD), so an XCD's blocks work on one or two pairs and that pair's A
+//     rows (1.3 MB) and E rows stay in its L2.
+//   * The tile loop runs two accumulator sets: tile t+1's four MFMAs issue
+//     before tile t's 64 decision VALU, so one wave keeps the matrix pipe and
+//     the vector issue busy together (scripts/probe_tile.hip: 247 -> 213 SIMD
+//     cycles per tile at 3 waves per SIMD).  Spans are 32 tiles: the 32-bit
+//     decision strings are full, and a run's fixed costs (A rows, queue,
+//     float64 drain, count reduction) spread over 32 tiles instead of 24.
+//   * The next run's A rows load right after the tile loop, under the
+//     queue / drain / reduction of the current run.
+//
+// Registers (gfx950, 3 waves per SIMD = 168 VGPRs): 2 x 48 accumulators + 16
+// A + 12 B + 32 decision strings in the loop.
+#ifndef SFM_MF2_SCHED
+#define SFM_MF2_SCHED 1
+#endif
+#ifndef SFM_MF2_SPAN
+#define SFM_MF2_SPAN 1024
+#endif
+constexpr int kMf2Waves = 12;                  // 3 per SIMD
+constexpr int kMf2Span = SFM_MF2_SPAN;         // points per staged span
+constexpr int kMf2Tiles = kMf2Span / 32;       // tiles per span (every run decides all of them)
+constexpr int kMf2Queue = 512;                 // undecided entries per wave and drain window
+static_assert(kMf2Tiles <= 32 && kMf2Tiles % 2 == 0, "32-bit decision strings, tiles in pairs");
+
+#ifdef SFM_MF_STATS
+// experiment builds only: [0] undecided evaluations, [1] evaluations decided by the tile loop
+__device__ unsigned long long g_mf2_stats[2];
+extern "C" int sfm_experiment_mf_stats(unsigned long long* out, int reset) {
+  if (reset) {
+    unsigned long long z[2] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_mf2_stats), z, sizeof(z)) == hipSuccess ? 0 : 2;
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mf2_stats), 16) == hipSuccess ? 0 : 2;
+}
+#endif
+
+// The float64 test of queued (row, span-relative point) entries; E rows from
+// the candidate records in global memory (L1/L2-resident: the tile's 32
+// records), points from the staged span.
+__device__ __forceinline__ void mf2_drain(const double* __restrict__ Erow0, const double4* __restrict__ spts,
+                                          const ScoreConsts& kc, int lane, int32_t* cnt, const uint32_t* q, int qn) {
+#pragma unroll 1
+  for (int i = lane; i < qn; i += 64) {
+    const uint32_t e = q[i];
+    const int c = (int)(e >> 24), r = (int)(e & 0xffffffu);
+    if (inlier_f64v(Erow0 + (size_t)c * kCandStride, spts[r], kc)) atomicAdd(&cnt[c], 1);
+  }
+}
+
+// mf_tile_decide with each register's decisions kept together (scheduling
+// barriers): the compiler otherwise hoists all 32 FMAs of a tile ahead of the
+// shifts, 32 temporaries that the two accumulator sets leave no room for
+__device__ __forceinline__ void mf2_decide(const MfAcc& r, uint32_t (&s1)[16], uint32_t (&s2)[16]) {
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const float z1 = __builtin_fmaf(r.a[g], r.a[g], -r.lo[g]);
+    const float z2 = __builtin_fmaf(-r.a[g], r.a[g], r.hi[g]);
+    s1[g] = __builtin_amdgcn_alignbit(s1[g], __float_as_uint(z1), 31);
+    s2[g] = __builtin_amdgcn_alignbit(s2[g], __float_as_uint(z2), 31);
+#if SFM_MF2_SCHED
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
+}
+
+// the lane id, recomputed where it is used (v_mbcnt) instead of kept live
+// across the tile loop, where every VGPR is taken
+__device__ __forceinline__ int mf2_lane() {
+  int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
+template <class Src>
+__global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_score_mf2(
+    const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
+    const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
+    int32_t* __restrict__ cntR, ScoreConsts kc) {
+  __shared__ __attribute__((aligned(16))) _Float16 s_frag[kMf2Tiles][3][64][8];
+  __shared__ double4 s_pts[kMf2Span];
+  __shared__ uint32_t s_queue[kMf2Waves][kMf2Queue];
+  __shared__ int32_t s_cnt[kMf2Waves][kKC];                  // float64 drain counts
+  __shared__ long long s_first[SFM_MAX_BATCH + 1];           // first unit of each pair
+  __shared__ int32_t s_tiles[SFM_MAX_BATCH];                 // candidate tiles per pair
+  __shared__ int32_t s_ctot[SFM_MAX_BATCH];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hl = lane >> 5, rl = lane & 31;
+  if (tid == 0) {
+    long long acc = 0;
+    for (int b = 0; b < batch; ++b) {
+      const int ct = cand_total[b];
+      const int tiles = (ct + kKC - 1) / kKC;
+      const long long spans = (max(pp.test[b], pp.rtest[b]) + kMf2Span - 1) / kMf2Span;
+      s_first[b] = acc;
+      s_tiles[b] = tiles;
+      s_ctot[b] = ct;
+      acc += spans * tiles;
+    }
+    s_first[batch] = acc;
+  }
+  for (int i = tid; i < kMf2Waves * kKC; i += kMf2Waves * 64) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  // XCD-aware contiguous ranges: workgroup ids are dealt round-robin over the
+  // 8 XCDs, so id % 8 names the XCD; logical block = XCD-major.
+  const int G = gridDim.x;
+  const int per_xcd = G / 8;
+  const int logical = (G % 8 == 0) ? (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const long long U = s_first[batch];
+  const long long u_beg = U * logical / G, u_end = U * (logical + 1) / G;
+  int32_t* cnt = s_cnt[wv];
+  uint32_t* queue = s_queue[wv];
+  const _Float16* fr = &s_frag[0][0][0][0];
+  constexpr int kTileHalves = 3 * 64 * 8;
+  int b = 0;
+  long long u = u_beg;
+  mf_half8 A1, A2, AL, AH;
+  // A rows of candidate tile k of pair b (absent rows: every evaluation a decided outlier)
+  auto load_rows = [&](int bb, int k) {
+    const int ln = mf2_lane();
+    const int lh = ln >> 5, lr = ln & 31;
+    const int c = k * kKC + lr;
+    if (c < s_ctot[bb]) {
+      const mf_half8* rec = reinterpret_cast<const mf_half8*>(candF + ((size_t)bb * cmax + c) * kMfRec);
+      A1 = rec[0 + lh];
+      A2 = rec[2 + lh];
+      AL = rec[4 + lh];
+      AH = rec[6 + lh];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        A1[j] = (_Float16)0.0f; A2[j] = (_Float16)0.0f; AL[j] = (_Float16)0.0f; AH[j] = (_Float16)0.0f;
+      }
+      if (lh == 0) {
+        AL[2] = (_Float16)(-1.0f); AH[2] = (_Float16)(-1.0f);
+      } else {
+        AL[6] = (_Float16)(-1.0f); AL[7] = (_Float16)(-1.0f);
+        AH[6] = (_Float16)(-1.0f); AH[7] = (_Float16)(-1.0f);
+      }
+    }
+  };
+  while (u < u_end) {
+    while (u >= s_first[b + 1]) ++b;
+    b = __builtin_amdgcn_readfirstlane(b);
+    const int tiles = s_tiles[b];
+    const long long local = u - s_first[b];
+    const int span = (int)(local / tiles);
+    const int k0 = (int)(local - (long long)span * tiles);
+    const int k1 = (int)min((long long)tiles, (long long)k0 + (u_end - u));   // this block's tiles of the span
+    const int p0 = span * kMf2Span;
+    const int np = min(max(pp.test[b], pp.rtest[b]) - p0, kMf2Span);     // live points of the span
+    // 1. stage the span: B fragments for every slot (dead slots: the decided-outlier sentinel)
+    for (int i = tid; i < kMf2Span; i += kMf2Waves * 64) {
+      const bool live = i < np;
+      const double4 v = src.load(b, live ? p0 + i : p0);
+      s_pts[i] = v;
+      mf_stage_point(v, live, &s_frag[i >> 5][0][0][0], i & 31);
+    }
+    lds_barrier();
+    // 2. this wave's candidate tiles of the span
+    int k = k0 + wv;
+    if (k < k1) load_rows(b, k);
+#pragma unroll 1
+    for (; k < k1; k += kMf2Waves) {
+      const int c0 = k * kKC;
+      uint32_t s1[16], s2[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) { s1[g] = 0u; s2[g] = 0u; }
+      {
+        // two accumulator sets: tile t+1's MFMAs beside tile t's decisions
+        // (the last pair peeled, so the loop body has no conditional MFMA)
+        MfB B = mf_load_b(fr, mf2_lane());
+        MfAcc ra = mf_tile_mfma(B, A1, A2, AL, AH), rb;
+#pragma unroll 1
+        for (int t = 0; t < kMf2Tiles - 2; t += 2) {
+          B = mf_load_b(fr + (size_t)(t + 1) * kTileHalves, mf2_lane());
+          rb = mf_tile_mfma(B, A1, A2, AL, AH);
+          mf2_decide(ra, s1, s2);
+          B = mf_load_b(fr + (size_t)(t + 2) * kTileHalves, mf2_lane());
+          ra = mf_tile_mfma(B, A1, A2, AL, AH);
+          mf2_decide(rb, s1, s2);
+        }
+        B = mf_load_b(fr + (size_t)(kMf2Tiles - 1) * kTileHalves, mf2_lane());
+        rb = mf_tile_mfma(B, A1, A2, AL, AH);
+        mf2_decide(ra, s1, s2);
+        mf2_decide(rb, s1, s2);
+      }
+      const int lane = mf2_lane(), hl = lane >> 5, rl = lane & 31;
+      // the next run's rows load under this run's queue, drain and reduction
+      const int kn = k + kMf2Waves;
+      if (kn < k1) load_rows(b, kn);
+      // 3. undecided evaluations -> the queue -> float64.  Bit j of a string
+      // is tile kMf2Tiles-1-j, point 32 (kMf2Tiles-1-j) + rl of the span.
+      int nl = 0;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) nl += __popc(~(s1[g] | s2[g]));
+      const int incl = mf_wave_scan(nl, lane);
+      const int qtotal = __builtin_amdgcn_readlane(incl, 63);
+#ifdef SFM_MF_STATS
+      if (lane == 0) {
+        atomicAdd(&g_mf2_stats[0], (unsigned long long)qtotal);
+        atomicAdd(&g_mf2_stats[1], (unsigned long long)kKC * kMf2Span);
+      }
+#endif
+      const double* Erow0 = candE + ((size_t)b * cmax + c0) * kCandStride;
+      for (int base = 0; base < qtotal; base += kMf2Queue) {
+        int pos = incl - nl - base;
+        if (qtotal <= kMf2Queue) {
+          uint32_t* q = queue + pos;
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            uint32_t uu = ~(s1[g] | s2[g]);
+            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+            while (uu) {
+              *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
+              uu &= uu - 1u;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            uint32_t uu = ~(s1[g] | s2[g]);
+            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+            while (uu) {
+              if (pos >= 0 && pos < kMf2Queue) queue[pos] = top - 32u * (uint32_t)__builtin_ctz(uu);
+              uu &= uu - 1u;
+              ++pos;
+            }
+          }
+        }
+        wave_sync();
+        mf2_drain(Erow0, s_pts, kc, lane, cnt, queue, min(kMf2Queue, qtotal - base));
+        wave_sync();
+      }
+      // 4. counts: popcounts of the inlier strings over the 32 points of each half + the float64 counts
+      int cT[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) cT[g] = __popc(s1[g]);
+      const int sumT = mf_half_reduce(cT, lane);
+      if ((lane & 1) == 0) {
+        const int c = mf_row((rl >> 1) & 15, hl);
+        const int d = sumT + cnt[c];
+        cnt[c] = 0;
+        if (d && c0 + c < s_ctot[b]) {
+          atomicAdd(cntT + (size_t)b * cmax + c0 + c, d);
+          atomicAdd(cntR + (size_t)b * cmax + c0 + c, d);
+        }
+      }
+      wave_sync();
+    }
+    u += k1 - k0;
+    lds_barrier();                                            // the span is re-staged next
+  }
+}
