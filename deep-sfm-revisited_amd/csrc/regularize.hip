@@ -566,6 +566,180 @@ __global__ __launch_bounds__(256) void k_to_channels_last_f4(const float* __rest
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// fp32 path (conv_precision = "fp32"): the same Conv3d layers at the
+// reference's precision, on v_mfma_f32_32x32x2_f32 (f32 operands, f32
+// accumulation; gfx950's f32 MFMA is an exact fmaf chain, so every product and
+// sum rounds as float32 arithmetic does -- only the summation order differs
+// from a CPU conv).  Activations are channels-last fp32 [B][D][H][W][C] (128 B
+// per voxel at C = 32), weights [27 taps][32 cout][Cin] fp32.
+//
+// k_conv3_f32: a block (4 waves) owns one depth slice d, 8 output rows x 64
+// columns; a wave owns 4 rows x 32 columns (four 32x32 accumulators).  K = 27
+// taps x Cin is staged per (dz, 16-channel quarter of a 32-channel chunk):
+// the 10 x 66 halo of plane d+dz-1 (64 B per pixel) and the 9 (dy, dx) weight
+// taps, 60.7 KB, two blocks per CU so one block's staging overlaps the other's
+// MFMAs.  An MFMA consumes k = 2 (lane half kh supplies channel 8 kh + j of
+// the quarter at k-step j); each lane reads its 8 channels of a pixel (or of a
+// cout row) as two ds_read_b128, 16-byte chunks XOR-swizzled by (p >> 2) & 3
+// so a 16-lane group of ds_read_b128 hits 16 distinct bank slots.  Per stage
+// and wave: 3 dx x 8 k-steps x 3 dy x 4 rows = 288 MFMAs (64 cycles each at
+// one wave per SIMD) against 3 x 6 input and 3 x 3 weight fragment pairs.
+// Out-of-range planes (dz at the volume's ends) contribute zeros and are not
+// staged at all.  The epilogue is k_conv3's in fp32: scale/bias, ReLU,
+// residual, float4 stores (or the single output channel as fp32 [B][D][H][W]).
+constexpr int kF32Ch = 16;                                   // channels per stage
+constexpr int kF32Pix = kF32Ch * 4;                          // 64 B per staged pixel
+constexpr int kF32InBytes = kHaloY * kHaloX * kF32Pix;       // 42,240
+constexpr int kF32WBytes = 9 * 32 * kF32Pix;                 // 18,432
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz4(int chunk, int p) { return chunk ^ ((p >> 2) & 3); }
+
+__global__ __launch_bounds__(kConvThreads, 2) void k_conv3_f32(
+    const float* __restrict__ in, int cin, const float* __restrict__ wpk, const float* __restrict__ scale,
+    const float* __restrict__ bias, const float* __restrict__ res, int relu, float* __restrict__ out,
+    float* __restrict__ out1, int D, int H, int W, int ntx, int nty, int nblk, int per_xcd) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds_in[kF32InBytes];
+  __shared__ __attribute__((aligned(16))) unsigned char lds_w[kF32WBytes];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int logical = (int)(blockIdx.x % kXcds) * per_xcd + (int)(blockIdx.x / kXcds);   // XCD-aware, d-fastest
+  if (logical >= nblk) return;
+  const int d = logical % D;
+  int rest = logical / D;
+  const int tx = rest % ntx;
+  rest /= ntx;
+  const int ty = rest % nty, b = rest / nty;
+  const int x0 = tx * kTileX, y0 = ty * kTileY;
+  const int r = lane & 31, kh = lane >> 5;
+  const int wrow = (wave >> 1) * 4, wcol = (wave & 1) * 32;
+  const int nq = cin / kF32Ch;
+  const int64_t plane = (int64_t)H * W;
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+    for (int i = 0; i < 16; ++i) acc[o][i] = 0.0f;
+
+  for (int dz = 0; dz < 3; ++dz) {
+    const int zd = d + dz - 1;
+    if (zd < 0 || zd >= D) continue;                         // zero padding: no contribution (block-uniform)
+    const float* pl = in + ((int64_t)b * D + zd) * plane * cin;
+    for (int q = 0; q < nq; ++q) {
+      __syncthreads();                                       // the previous stage's operand reads are done
+      // input halo: 10 rows x 66 pixels x 4 chunks of 16 B
+      for (int i = tid; i < kHaloY * kHaloX * 4; i += kConvThreads) {
+        const int c = i & 3, px = (i >> 2) % kHaloX, ry = (i >> 2) / kHaloX;
+        const int gx = x0 - 1 + px, gy = y0 - 1 + ry;
+        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (gx >= 0 && gx < W && gy >= 0 && gy < H)
+          v = *reinterpret_cast<const float4*>(pl + ((int64_t)gy * W + gx) * cin + q * kF32Ch + c * 4);
+        *reinterpret_cast<float4*>(lds_in + (ry * kHaloX + px) * kF32Pix + swz4(c, px) * 16) = v;
+      }
+      // weights: 9 (dy, dx) taps x 32 cout x 4 chunks
+      for (int i = tid; i < 9 * 32 * 4; i += kConvThreads) {
+        const int c = i & 3, co = (i >> 2) & 31, t = i >> 7;
+        const float4 v = *reinterpret_cast<const float4*>(wpk + ((int64_t)(dz * 9 + t) * 32 + co) * cin + q * kF32Ch + c * 4);
+        *reinterpret_cast<float4*>(lds_w + (t * 32 + co) * kF32Pix + swz4(c, co) * 16) = v;
+      }
+      __syncthreads();
+#pragma unroll 1
+      for (int dx = 0; dx < 3; ++dx) {
+        const int p = wcol + r + dx;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {                        // channels 8 kh + 4 e .. + 3
+          const int ch = 2 * kh + e;
+          f32x4 wf[3], xf[6];
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy)
+            wf[dy] = *reinterpret_cast<const f32x4*>(lds_w + ((dy * 3 + dx) * 32 + r) * kF32Pix + swz4(ch, r) * 16);
+#pragma unroll
+          for (int ir = 0; ir < 6; ++ir)
+            xf[ir] = *reinterpret_cast<const f32x4*>(lds_in + ((wrow + ir) * kHaloX + p) * kF32Pix + swz4(ch, p) * 16);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+              for (int o = 0; o < 4; ++o)
+                acc[o] = __builtin_amdgcn_mfma_f32_32x32x2f32(wf[dy][j], xf[o + dy][j], acc[o], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // epilogue: lane holds pixel r, couts 8q + 4kh + (0..3) in acc[.][4q .. 4q+3]
+  const int x = x0 + wcol + r;
+  if (x >= W) return;
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const int y = y0 + wrow + o;
+    if (y >= H) break;
+    const int64_t pix = ((int64_t)b * D + d) * plane + (int64_t)y * W + x;
+    if (out1) {
+      if (kh == 0) out1[pix] = __builtin_fmaf(acc[o][0], scale[0], bias[0]);
+      continue;
+    }
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int co = 8 * qq + 4 * kh;
+      const float4 sc = *reinterpret_cast<const float4*>(scale + co);
+      const float4 bi = *reinterpret_cast<const float4*>(bias + co);
+      float4 v = make_float4(__builtin_fmaf(acc[o][4 * qq + 0], sc.x, bi.x), __builtin_fmaf(acc[o][4 * qq + 1], sc.y, bi.y),
+                             __builtin_fmaf(acc[o][4 * qq + 2], sc.z, bi.z), __builtin_fmaf(acc[o][4 * qq + 3], sc.w, bi.w));
+      if (relu) {
+        v.x = fmaxf(v.x, 0.0f);
+        v.y = fmaxf(v.y, 0.0f);
+        v.z = fmaxf(v.z, 0.0f);
+        v.w = fmaxf(v.w, 0.0f);
+      }
+      if (res) {
+        const float4 rv = *reinterpret_cast<const float4*>(res + pix * 32 + co);
+        v.x += rv.x;
+        v.y += rv.y;
+        v.z += rv.z;
+        v.w += rv.w;
+      }
+      *reinterpret_cast<float4*>(out + pix * 32 + co) = v;
+    }
+  }
+}
+
+// [B][C][P] (fp32 or bf16) -> [B][P][C] fp32 through a 64-pixel x 64-channel
+// LDS tile: coalesced reads along P per channel, 16-byte writes along C.
+template <typename T>
+__global__ __launch_bounds__(256) void k_to_channels_last_f32(const T* __restrict__ in, int C, int64_t P,
+                                                              float* __restrict__ out) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.y;
+  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    __syncthreads();
+    for (int i = tid; i < 64 * 64; i += 256) {
+      const int px = i & 63, c = i >> 6;
+      const int64_t p = p0 + px;
+      float v = 0.0f;
+      if (p < P && c0 + c < C) {
+        if constexpr (sizeof(T) == 4) v = in[((int64_t)b * C + c0 + c) * P + p];
+        else v = bf2f(in[((int64_t)b * C + c0 + c) * P + p]);
+      }
+      tile[c][px] = v;
+    }
+    __syncthreads();
+    const int cw = min(64, C - c0);
+    for (int i = tid; i < 64 * (cw / 4); i += 256) {
+      const int g = i % (cw / 4), px = i / (cw / 4);
+      const int64_t p = p0 + px;
+      if (p >= P) continue;
+      *reinterpret_cast<float4*>(out + ((int64_t)b * P + p) * C + c0 + g * 4) =
+          make_float4(tile[g * 4][px], tile[g * 4 + 1][px], tile[g * 4 + 2][px], tile[g * 4 + 3][px]);
+    }
+  }
+}
+
 }  // namespace
 }  // namespace sfm
 
@@ -643,6 +817,51 @@ int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int chann
   else
     hipLaunchKernelGGL(k_to_channels_last<unsigned short>, grid, dim3(256), 0, s, (const unsigned short*)in, channels,
                        plane, (unsigned short*)out);
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+int sfm_conv3_f32(const float* in, int batch, int cin, int depth, int h, int w, const float* weights,
+                  const float* scale, const float* bias, const float* residual, int relu, int cout, float* out,
+                  void* stream) {
+  SFM_REQUIRE(in && weights && scale && bias && out, "null pointer argument");
+  SFM_REQUIRE(cin == 32 || cin == 64, "cin must be 32 or 64");
+  SFM_REQUIRE(cout == 32 || cout == 1, "cout must be 32 or 1");
+  SFM_REQUIRE(cout == 32 || residual == nullptr, "residual needs cout 32");
+  SFM_REQUIRE(batch >= 1 && depth >= 1 && h >= 1 && w >= 1, "invalid conv shape");
+  SFM_REQUIRE(in != out && (residual == nullptr || residual != out), "conv output must not alias its inputs");
+  SFM_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)weights & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                  ((uintptr_t)residual & 15) == 0,
+              "conv operands must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps("conv3_f32", s);
+  const int ntx = (w + kTileX - 1) / kTileX;
+  const int nty = (h + kTileY - 1) / kTileY;
+  const int64_t nblk = (int64_t)ntx * nty * batch * depth;
+  SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
+  const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
+  hipLaunchKernelGGL(k_conv3_f32, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, in, cin, weights,
+                     scale, bias, residual, relu, cout == 32 ? out : nullptr, cout == 1 ? out : nullptr, depth, h, w,
+                     ntx, nty, (int)nblk, per_xcd);
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channels, int64_t plane, float* out,
+                             void* stream) {
+  SFM_REQUIRE(in && out, "null pointer argument");
+  SFM_REQUIRE(in_dtype == 0 || in_dtype == 1, "in_dtype must be 0 (float32) or 1 (bfloat16)");
+  SFM_REQUIRE(batch >= 1 && batch <= 65535 && channels >= 4 && channels % 4 == 0 && plane >= 1,
+              "invalid channels-last shape (channels must be a multiple of 4)");
+  SFM_REQUIRE(((uintptr_t)out & 15) == 0, "output must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  ProfScope ps("to_channels_last", s);
+  dim3 grid((unsigned)((plane + 63) / 64), batch);
+  if (in_dtype == 0)
+    hipLaunchKernelGGL(k_to_channels_last_f32<float>, grid, dim3(256), 0, s, (const float*)in, channels, plane, out);
+  else
+    hipLaunchKernelGGL(k_to_channels_last_f32<unsigned short>, grid, dim3(256), 0, s, (const unsigned short*)in,
+                       channels, plane, out);
   SFM_LAUNCHED();
   return SFM_OK;
 }

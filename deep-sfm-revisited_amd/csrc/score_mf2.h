@@ -103,6 +103,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   __shared__ long long s_first[SFM_MAX_BATCH + 1];           // first unit of each pair
   __shared__ int32_t s_tiles[SFM_MAX_BATCH];                 // candidate tiles per pair
   __shared__ int32_t s_ctot[SFM_MAX_BATCH];
+  __shared__ int32_t s_claim;                                // next candidate tile of the span to claim
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int hl = lane >> 5, rl = lane & 31;
   if (tid == 0) {
@@ -134,6 +135,13 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   int b = 0;
   long long u = u_beg;
   mf_half8 A1, A2, AL, AH;
+#ifdef SFM_MF_STAMPS
+  // experiment builds (scripts/mf_stamps.py): [0] staging, [1] tile loop,
+  // [2] queue build, [3] float64 drain, [4] reduction + atomics, [5] span
+  // barriers, [6] A-row load issue, [7] runs
+  unsigned long long mf_t0_ = __builtin_amdgcn_s_memtime();
+  unsigned long long mf_acc_[kMfStamps] = {};
+#endif
   // A rows of candidate tile k of pair b (absent rows: every evaluation a decided outlier)
   auto load_rows = [&](int bb, int k) {
     const int ln = mf2_lane();
@@ -169,18 +177,32 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     const int p0 = span * kMf2Span;
     const int np = min(max(pp.test[b], pp.rtest[b]) - p0, kMf2Span);     // live points of the span
     // 1. stage the span: B fragments for every slot (dead slots: the decided-outlier sentinel)
+    if (tid == 0) s_claim = 0;
     for (int i = tid; i < kMf2Span; i += kMf2Waves * 64) {
       const bool live = i < np;
       const double4 v = src.load(b, live ? p0 + i : p0);
       s_pts[i] = v;
       mf_stage_point(v, live, &s_frag[i >> 5][0][0][0], i & 31);
     }
+    MF_STAMP(0);
     lds_barrier();
-    // 2. this wave's candidate tiles of the span
-    int k = k0 + wv;
+    MF_STAMP(5);
+    // 2. the span's candidate tiles, claimed one run at a time from an LDS
+    // counter: the three waves of a SIMD progress at very different rates
+    // (issue arbitration favours the oldest), so a static split left the
+    // younger waves' tail for the others to wait out at the span barrier
+    auto claim = [&]() {
+      int j = 0;
+      if (mf2_lane() == 0) j = atomicAdd(&s_claim, 1);
+      return k0 + __builtin_amdgcn_readfirstlane(__shfl(j, 0, 64));
+    };
+    int k = claim();
     if (k < k1) load_rows(b, k);
 #pragma unroll 1
-    for (; k < k1; k += kMf2Waves) {
+    while (k < k1) {
+#ifdef SFM_MF_STAMPS
+      mf_acc_[7] += 1;
+#endif
       const int c0 = k * kKC;
       uint32_t s1[16], s2[16];
 #pragma unroll
@@ -204,10 +226,12 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         mf2_decide(ra, s1, s2);
         mf2_decide(rb, s1, s2);
       }
+      MF_STAMP(1);
       const int lane = mf2_lane(), hl = lane >> 5, rl = lane & 31;
       // the next run's rows load under this run's queue, drain and reduction
-      const int kn = k + kMf2Waves;
+      const int kn = claim();
       if (kn < k1) load_rows(b, kn);
+      MF_STAMP(6);
       // 3. undecided evaluations -> the queue -> float64.  Bit j of a string
       // is tile kMf2Tiles-1-j, point 32 (kMf2Tiles-1-j) + rl of the span.
       int nl = 0;
@@ -248,9 +272,12 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           }
         }
         wave_sync();
+        MF_STAMP(2);
         mf2_drain(Erow0, s_pts, kc, lane, cnt, queue, min(kMf2Queue, qtotal - base));
         wave_sync();
+        MF_STAMP(3);
       }
+      MF_STAMP(2);
       // 4. counts: popcounts of the inlier strings over the 32 points of each half + the float64 counts
       int cT[16];
 #pragma unroll
@@ -266,8 +293,15 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         }
       }
       wave_sync();
+      MF_STAMP(4);
+      k = kn;
     }
     u += k1 - k0;
     lds_barrier();                                            // the span is re-staged next
+    MF_STAMP(5);
   }
+#ifdef SFM_MF_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < kMfStamps; ++i) atomicAdd(&g_mf_stamps[i], mf_acc_[i]);
+#endif
 }

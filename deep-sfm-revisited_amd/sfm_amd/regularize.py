@@ -10,8 +10,10 @@ its application at PSNet.py:159-165:
 
 ``CostRegularization.forward`` runs the 12 Conv3d layers as
 ``sfm_conv3_bf16`` launches (bf16 channels-last activations, fp32
-accumulation, BatchNorm3d folded in eval mode, ReLU and residual fused into
-the epilogue).  There is no PyTorch fallback: without libsfm_hip.so or a GPU
+accumulation; the fast option) or, with ``precision="fp32"``, as
+``sfm_conv3_f32`` launches (fp32 activations and weights on the f32 matrix
+cores: the reference's precision).  BatchNorm3d is folded in eval mode, ReLU
+and residual are fused into the epilogue.  There is no PyTorch fallback: without libsfm_hip.so or a GPU
 the call raises.
 """
 import math
@@ -111,11 +113,13 @@ class CostRegularization(nn.Module):
     def _key(self, device):
         return (str(device),) + tuple((t.data_ptr(), t._version) for t in list(self.parameters()) + list(self.buffers()))
 
-    def pack(self, device):
-        """Packed bf16 weights [27][32][Cin] and folded fp32 scale/bias per layer."""
-        key = self._key(device)
+    def pack(self, device, precision="bf16"):
+        """Packed weights [27][32][Cin] (bf16, or fp32 for precision "fp32")
+        and folded fp32 scale/bias per layer."""
+        key = self._key(device) + (precision,)
         if self._packed is not None and self._packed_key == key:
             return self._packed
+        wdt = torch.float32 if precision == "fp32" else torch.bfloat16
         packed = []
         with torch.no_grad():
             for conv, bn, relu, resid in self.layer_plan():
@@ -133,7 +137,7 @@ class CostRegularization(nn.Module):
                 bi = torch.zeros(32)
                 sc[:cout] = scale.cpu()
                 bi[:cout] = bias.cpu()
-                packed.append(dict(w=wp.to(device=device, dtype=torch.bfloat16).contiguous(),
+                packed.append(dict(w=wp.to(device=device, dtype=wdt).contiguous(),
                                    scale=sc.to(device), bias=bi.to(device), cin=cin, cout=cout, relu=relu,
                                    resid=resid))
         self._packed, self._packed_key = packed, key
@@ -141,8 +145,10 @@ class CostRegularization(nn.Module):
 
     def forward(self, cost, precision="bf16"):
         """cost [B, Cin, L, h, w] fp32 or bf16 (the sweep's volume) -> [B, 1, L, h, w] fp32.
-        ``precision``: "bf16" (bf16 activations and weights, fp32 accumulation)."""
-        if precision != "bf16":
+        ``precision``: "bf16" (bf16 activations and weights, fp32 accumulation:
+        sfm_conv3_bf16, the fast option) or "fp32" (fp32 activations, weights
+        and accumulation: sfm_conv3_f32, the reference's precision)."""
+        if precision not in ("bf16", "fp32"):
             raise ValueError(f"unknown conv precision {precision!r}")
         if not (isinstance(cost, torch.Tensor) and cost.is_cuda):
             raise RuntimeError("CostRegularization.forward needs a device tensor (HIP path, no CPU fallback)")
@@ -150,17 +156,21 @@ class CostRegularization(nn.Module):
             raise RuntimeError("cost must be a [B, C, L, h, w] float32 or bfloat16 tensor")
         cost = cost.contiguous()
         B, C, L, h, w = cost.shape
-        packed = self.pack(cost.device)
+        packed = self.pack(cost.device, precision)
         if C != packed[0]["cin"]:
             raise RuntimeError(f"cost has {C} channels, the first layer expects {packed[0]['cin']}")
         lib = _lib.load()
         dev = cost.device
+        fp32 = precision == "fp32"
+        adt = torch.float32 if fp32 else torch.bfloat16
+        to_cl = lib.sfm_to_channels_last_f32 if fp32 else lib.sfm_to_channels_last_bf16
+        conv = lib.sfm_conv3_f32 if fp32 else lib.sfm_conv3_bf16
         with torch.cuda.device(dev):
             stream = _lib.stream_ptr(dev)
-            x = torch.empty((B, L, h, w, C), dtype=torch.bfloat16, device=dev)
-            _lib.check(lib.sfm_to_channels_last_bf16(_lib.ptr(cost), 0 if cost.dtype == torch.float32 else 1, B, C,
-                                                     L * h * w, _lib.ptr(x), stream), "sfm_to_channels_last_bf16")
-            bufs = [torch.empty((B, L, h, w, 32), dtype=torch.bfloat16, device=dev) for _ in range(3)]
+            x = torch.empty((B, L, h, w, C), dtype=adt, device=dev)
+            _lib.check(to_cl(_lib.ptr(cost), 0 if cost.dtype == torch.float32 else 1, B, C, L * h * w, _lib.ptr(x),
+                             stream), "sfm_to_channels_last")
+            bufs = [torch.empty((B, L, h, w, 32), dtype=adt, device=dev) for _ in range(3)]
             out = torch.empty((B, 1, L, h, w), dtype=torch.float32, device=dev)
             cur, keep = x, None           # keep: the block input of a residual pair (cost0)
             for li, lay in enumerate(packed):
@@ -169,11 +179,10 @@ class CostRegularization(nn.Module):
                 else:
                     dst = next(bb for bb in bufs if bb is not cur and bb is not keep)
                 res = keep if lay["resid"] else None
-                rc = lib.sfm_conv3_bf16(_lib.ptr(cur), B, lay["cin"], L, h, w, _lib.ptr(lay["w"]),
-                                        _lib.ptr(lay["scale"]), _lib.ptr(lay["bias"]),
-                                        None if res is None else _lib.ptr(res), 1 if lay["relu"] else 0,
-                                        lay["cout"], _lib.ptr(dst), stream)
-                _lib.check(rc, "sfm_conv3_bf16")
+                rc = conv(_lib.ptr(cur), B, lay["cin"], L, h, w, _lib.ptr(lay["w"]), _lib.ptr(lay["scale"]),
+                          _lib.ptr(lay["bias"]), None if res is None else _lib.ptr(res), 1 if lay["relu"] else 0,
+                          lay["cout"], _lib.ptr(dst), stream)
+                _lib.check(rc, "sfm_conv3_f32" if fp32 else "sfm_conv3_bf16")
                 # cost0 after dres0 (layer 1) and after every residual add is the next block's input
                 if li == 1 or lay["resid"]:
                     keep = dst
@@ -182,7 +191,7 @@ class CostRegularization(nn.Module):
 
 
 def psnet_depth(ref_fea, tgt_fea, pose, intrinsics, intrinsics_inv, regularizer, nlabel, min_depth=1.0,
-                out_hw=None, predict_by_depth=False, cost_dtype=torch.float32):
+                out_hw=None, predict_by_depth=False, cost_dtype=torch.float32, precision=None):
     """PSNet's single-target depth path at feature resolution, PSNet.py:130-216
     without the context network (cfg.PSNET_CONTEXT off): plane sweep ->
     dres/classify -> trilinear upsample, softmax, disparity regression.
@@ -191,7 +200,7 @@ def psnet_depth(ref_fea, tgt_fea, pose, intrinsics, intrinsics_inv, regularizer,
     K4, Ki4 = quarter_intrinsics(intrinsics, intrinsics_inv)
     cost = plane_sweep_cost(ref_fea, tgt_fea, pose, K4, Ki4, nlabel, min_depth, dtype=cost_dtype,
                             predict_by_depth=predict_by_depth)
-    costs = regularizer(cost)
+    costs = regularizer(cost) if precision is None else regularizer(cost, precision=precision)
     B = costs.shape[0]
     h, w = costs.shape[-2:]
     H, W = out_hw if out_hw is not None else (4 * h, 4 * w)

@@ -294,6 +294,25 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
 int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
                               void* stream);
 
+/* The same layer at the reference's precision (conv_precision "fp32"):
+ * float32 operands on v_mfma_f32_32x32x2_f32 (an exact fmaf chain: products
+ * and sums round as float32 arithmetic; only the summation order differs from
+ * PSNet's own Conv3d, models/PSNet.py:79-102).
+ *   in [dev] batch x depth x h x w x cin float32 (channels-last), cin 32 or 64;
+ *   weights [dev] 27 x 32 x cin float32 (layout as sfm_conv3_bf16);
+ *   scale, bias [dev] 32 float32; residual [dev] like out or NULL;
+ *   out [dev] batch x depth x h x w x 32 float32 (cout 32), or
+ *       batch x depth x h x w float32 (cout 1).  All 16-byte aligned. */
+int sfm_conv3_f32(const float* in, int batch, int cin, int depth, int h, int w, const float* weights,
+                  const float* scale, const float* bias, const float* residual, int relu, int cout, float* out,
+                  void* stream);
+
+/* [batch][channels][plane] float32 (in_dtype 0) or bfloat16 (1) ->
+ * [batch][plane][channels] float32 (channels a multiple of 4): the sweep's
+ * cost volume into sfm_conv3_f32's layout. */
+int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channels, int64_t plane, float* out,
+                             void* stream);
+
 /* Tuning knobs (process-wide; every key, its accepted values and default):
  *
  *   launch shape only -- outputs are bit-identical for every value:

@@ -1,5 +1,8 @@
-"""Experiment: per-phase cycle split of k_score_mf (library built with
--DSFM_MF_STAMPS into scripts/exp/, selected with SFM_HIP_LIB)."""
+"""Experiment: per-phase cycle split of k_score_mf / k_score_mf2 (library
+built with -DSFM_MF_STAMPS into scripts/exp/, selected with SFM_HIP_LIB;
+argument: the score_mf tuning value, default 2).  For k_score_mf2 an "item"
+is one (span, candidate tile) run of a wave; "setup+staging" is the span
+staging, "block barrier" the span barriers, "prefetch issue" the A rows."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "deep-sfm-revisited_amd"))
@@ -9,8 +12,9 @@ from sfm_amd.pipeline import TwoViewHotPath
 dev = torch.device("cuda", 0)
 flow, K, _, _ = synth.kitti_pair_batch(8, seed=1000, device=dev)
 hp = TwoViewHotPath(8, (376, 1242), (94, 311), 32, 128, 8, 1e-4, 1.0, True, 0.6, device=dev)
-hp.pose(flow, K); torch.cuda.synchronize()
 lib = _lib.load()
+_lib.tune("score_mf", int(sys.argv[1]) if len(sys.argv) > 1 else 2)
+hp.pose(flow, K); torch.cuda.synchronize()
 out = (ctypes.c_ulonglong * 8)()
 lib.sfm_experiment_mf_stamps(out, 1)
 _lib.profile_reset(); _lib.profile_enable(True)
