@@ -50,6 +50,7 @@ PEAK_FP64_TFLOPS = 78.6      # MI355X fp64 vector spec
 PEAK_FP32_TFLOPS = 157.3     # MI355X fp32 vector spec (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0    # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 PEAK_F16_TFLOPS = 2500.0     # MI355X dense f16 MFMA (same rate as bf16; no sparsity)
+PEAK_F32_MFMA_TFLOPS = 157.3 # MI355X f32 MFMA (v_mfma_f32_32x32x2_f32 = the f32 vector rate; MI355X_MICROARCH.md)
 FLOP_PER_EVAL = 50           # Ex, xE, x'Ex, sqrt, div, |.|
 MF_MFMA_FLOP_PER_EVAL = 128  # k_score_mf: 4 x v_mfma_f32_32x32x16_f16 (32768 FLOP each) per 32x32 evaluations
 
@@ -209,33 +210,36 @@ def cpu_baseline(flow, K, ref_fea, tgt_fea, pose, args, n_pts=None, keypoints=No
     return out
 
 
-def regularize_roofline(cost, steps=3):
-    """PSNet's 12-layer 3-D cost regularisation (sfm_conv3_bf16) on the first
-    pair of the last step's cost volume, after the timed region.  Not part of
-    ``value`` (the metric's path ends at the cost volume); reported so the
-    MFMA kernel's roofline is measured live beside the path's."""
+def regularize_roofline(cost, steps=3, precision="bf16"):
+    """PSNet's 12-layer 3-D cost regularisation on the first pair of the last
+    step's cost volume, after the timed region: sfm_conv3_bf16 (bf16 MFMA,
+    the fast option) or sfm_conv3_f32 (precision "fp32": f32 MFMA, the
+    reference's precision).  Not part of ``value`` (the metric's path ends at
+    the cost volume); reported so the MFMA kernels' rooflines are measured
+    live beside the path's."""
     import torch
     from sfm_amd import _lib
     from sfm_amd.regularize import CostRegularization
     torch.manual_seed(0)
     reg = CostRegularization(cost.shape[1]).to(cost.device).eval()
     one = cost[:1]
-    reg(one)
+    reg(one, precision=precision)
     torch.cuda.synchronize(cost.device)
     _lib.profile_reset()
     _lib.profile_enable(True)
     for _ in range(steps):
-        reg(one)
+        reg(one, precision=precision)
     torch.cuda.synchronize(cost.device)
     _lib.profile_enable(False)
-    ms, n = _lib.profile_read("conv3")
+    ms, n = _lib.profile_read("conv3" if precision == "bf16" else "conv3_f32")
     _, L, h, w = one.shape[1:]
     vox = L * h * w
     flop = 2 * vox * 27 * (one.shape[1] * 32 + 10 * 32 * 32 + 32)
     per_stack = ms / steps
     tf = flop / (per_stack * 1e-3) / 1e12
-    return {"kernel": "conv3 x12 (PSNet dres0..classify, bf16 MFMA)", "bound": "mfma-bf16", "achieved": round(tf, 1),
-            "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(tf / PEAK_BF16_TFLOPS, 4),
+    peak = PEAK_BF16_TFLOPS if precision == "bf16" else PEAK_F32_MFMA_TFLOPS
+    return {"kernel": f"conv3 x12 (PSNet dres0..classify, {precision} MFMA)", "bound": f"mfma-{precision}",
+            "achieved": round(tf, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
             "avg_launch_ms": round(ms / max(n, 1), 4), "ms_per_stack": round(per_stack, 4),
             "work": f"{flop} FLOP per stack (1 pair, L={L}, {h}x{w}; 2*27*Cin*Cout per voxel and layer)",
             "note": "not part of value: the CNN after the measured path, timed after it"}
@@ -410,10 +414,11 @@ def _main_gpu(args, dist):
                          "via": "dist.gather_rows (all_gather of E[9], P[12], inliers per pair)"},
         }
         if world == 1 and not args.no_regularize and hp.cost.dtype in (torch.float32, torch.bfloat16):
-            try:
-                out["roofline_regularize"] = regularize_roofline(hp.cost)
-            except Exception as e:   # extra information, never the metric
-                out["roofline_regularize"] = {"error": repr(e)}
+            for prec, key in (("bf16", "roofline_regularize"), ("fp32", "roofline_regularize_fp32")):
+                try:
+                    out[key] = regularize_roofline(hp.cost, steps=3 if prec == "bf16" else 2, precision=prec)
+                except Exception as e:   # extra information, never the metric
+                    out[key] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
             try:
                 out["cpu_baseline"] = cpu_baseline(flow, K, ref_fea, tgt_fea, P.float(), args,

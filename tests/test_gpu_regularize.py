@@ -350,15 +350,18 @@ def test_psnet_golden_end_to_end_fp32(cuda, golden):
     map (psnet.npz).
     * from the reference's own cost volume (regularisation + head only):
       logits within 1e-5 (relative L2), depth median <= 1e-5, max <= 1e-3;
-    * from the features (our sweep too): median <= 1e-4 (north_star's bar),
-      99.9 % of the pixels within 1e-3.  The few others sit where a sample
-      lands on the warp's |xn| = 1 clamp (inverse_warp.py:63-66): a last-bit
-      difference in the projected coordinate there switches a bilinear tap
-      between the feature and zero padding (the sweep's own 1e-4 bound,
-      test_gpu_sweep.py), which moves that pixel's soft-argmin; the largest
-      measured is 5.5 % (bar 0.1)."""
+    * from the features (our sweep too): median <= 1e-4 (north_star's bar).
+      The sweep is bit-identical to the oracle restatement (oracle/sweep.py),
+      which differs from the reference's grid_sample in the last bit of ~5 %
+      of the warped entries (its own summation order; the fixture's random-init
+      features reach 7e5).  This random-init PSNet amplifies such 1-ulp input
+      changes to > 1e-3 of the depth at ~12 % of the pixels (max ~5.5 %): the
+      CPU reference chain itself, fed the oracle's cost instead of its own,
+      moves just as much (asserted below), while the GPU path fed the same
+      cost as the CPU chain agrees with it to <= 1e-3 everywhere."""
     from sfm_amd.depth import depth_head
     from sfm_amd.regularize import psnet_depth
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
     g, m = _psnet_golden(golden)
     inp, out = g["input"], g["out"]
     L = int(inp["nlabel"])
@@ -366,18 +369,26 @@ def test_psnet_golden_end_to_end_fp32(cuda, golden):
     md = float(inp["min_depth"])
     d = lambda k: torch.from_numpy(k).to(cuda)
     want = torch.from_numpy(out["depth_init"])
+    rel = lambda a, b: ((a - b).abs() / b.abs()).flatten()
     # 1. regularisation + head on the reference's cost volume
     logits = m.to(cuda)(d(out["cost"]), precision="fp32")
     cls = torch.from_numpy(out["classify"])
     rl = float((logits.cpu() - cls).norm() / cls.norm())
-    d1 = depth_head(logits, L, md, out_hw=hw).cpu()
-    rel1 = ((d1 - want).abs() / want.abs()).flatten()
-    msg1 = (rl, float(rel1.median()), float(rel1.max()))
-    assert rl <= 1e-5 and float(rel1.median()) <= 1e-5 and float(rel1.max()) <= 1e-3, msg1
+    r1 = rel(depth_head(logits, L, md, out_hw=hw).cpu(), want)
+    msg1 = (rl, float(r1.median()), float(r1.max()))
+    assert rl <= 1e-5 and float(r1.median()) <= 1e-5 and float(r1.max()) <= 1e-3, msg1
     # 2. the whole path from the features
     got = psnet_depth(d(out["ref_fea"]), d(out["tgt_fea"]), d(inp["pose_rescaled"])[:, 0], d(inp["K"]),
                       d(inp["Kinv"]), m.to(cuda), L, md, out_hw=hw, precision="fp32").cpu()
-    rel = ((got - want).abs() / want.abs()).flatten()
-    msg = (float(rel.median()), float(rel.max()), float((rel > 1e-3).float().mean()))
-    assert float(rel.median()) <= 1e-4, msg
-    assert float((rel > 1e-3).float().mean()) <= 1e-3 and float(rel.max()) <= 0.1, msg
+    r2 = rel(got, want)
+    assert float(r2.median()) <= 1e-4, (float(r2.median()), float(r2.max()))
+    # 3. the same cost on both sides: our sweep's volume (== the oracle's) through the CPU reference chain
+    K4, Ki4 = quarter_intrinsics(d(inp["K"]), d(inp["Kinv"]))
+    cost = plane_sweep_cost(d(out["ref_fea"]), d(out["tgt_fea"]), d(inp["pose_rescaled"])[:, 0], K4, Ki4, L, md)
+    m = m.cpu()
+    want_same = S.depth_head(R.regularize_fp32(m, cost.cpu()), L, md, out_hw=hw)
+    r3 = rel(got, want_same)
+    assert float(r3.median()) <= 1e-5 and float(r3.max()) <= 1e-3, (float(r3.median()), float(r3.max()))
+    # the fixture's own sensitivity: the CPU chain from the two costs (1-ulp apart) differs as much as r2
+    r4 = rel(want_same, want)
+    assert float((r4 > 1e-3).float().mean()) >= 0.5 * float((r2 > 1e-3).float().mean())
