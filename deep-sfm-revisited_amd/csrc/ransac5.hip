@@ -1592,6 +1592,71 @@ __global__ void k_keypoint_points(const float* __restrict__ flow, int H, int W, 
 #include "score_mf.h"
 #include "score_mf2.h"
 
+// The score-kernel choice (shared by the RANSAC driver and
+// sfm_score_essentials): the split-f16 matrix-core scorers when the threshold
+// and precision allow, else the float32 / float64 VALU scorers.
+struct ScoreBufs {
+  int32_t* cand_total;
+  double* candE;
+  _Float16* candF;
+  int32_t* cntT;
+  int32_t* cntR;
+};
+
+template <class Src>
+static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cmax, const ScoreBufs& w,
+                           const ScoreConsts& kc, const MfParams& mp, bool use_mf, bool same, int prec, bool fast,
+                           bool fast32, int cus, int grid, hipStream_t s) {
+  if (use_mf) {
+    hipLaunchKernelGGL(k_mf_cands, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax, w.cand_total, w.candE,
+                       w.candF, mp);
+    const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
+    if (same && tuning().score_mf == 2)
+      hipLaunchKernelGGL(k_score_mf2<Src>, dim3(std::max(1, cus)), dim3(kMf2Waves * 64), 0, s, src, pp, bc, cmax,
+                         w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
+    else if (same)
+      hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
+                         w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
+    else
+      hipLaunchKernelGGL((k_score_mf<Src, false>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
+                         w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
+  } else if (prec == 32)
+    hipLaunchKernelGGL((k_score<false, Src, 32>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
+                       w.cand_total, w.candE, w.cntT, w.cntR, kc);
+  else if (prec == 16)
+    hipLaunchKernelGGL((k_score<false, Src, 16>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
+                       w.cand_total, w.candE, w.cntT, w.cntR, kc);
+  else if (fast32 && same && tuning().score_mfma)
+    hipLaunchKernelGGL(k_score_mx<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax, w.cand_total,
+                       w.candE, w.cntT, w.cntR, kc);
+  else if (fast32)
+    hipLaunchKernelGGL(k_score32<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax, w.cand_total,
+                       w.candE, w.cntT, w.cntR, kc);
+  else if (fast)
+    hipLaunchKernelGGL((k_score<true, Src>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
+                       w.cand_total, w.candE, w.cntT, w.cntR, kc);
+  else
+    hipLaunchKernelGGL((k_score<false, Src>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
+                       w.cand_total, w.candE, w.cntT, w.cntR, kc);
+}
+
+// Candidate records of given essential matrices (sfm_score_essentials): E,
+// the float64 guard constant and the float32 constants, as k_cand writes them.
+__global__ __launch_bounds__(256) void k_fill_cands(const double* __restrict__ E, int ncand, int cmax,
+                                                    double guard_g, double thr, int fast32,
+                                                    double* __restrict__ candE, int32_t* __restrict__ cand_total) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c == 0) cand_total[b] = ncand;
+  if (c >= ncand) return;
+  double* dst = candE + ((size_t)b * cmax + c) * kCandStride;
+  const double* src = E + ((size_t)b * ncand + c) * 9;
+#pragma unroll
+  for (int e = 0; e < 9; ++e) dst[e] = src[e];
+  dst[9] = guard_constant(dst, guard_g);
+  fp32_constants(dst, thr, fast32 != 0, reinterpret_cast<float*>(dst + 10));
+}
+
 template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
@@ -1662,37 +1727,8 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   }
   {
     ProfScope ps("ransac_score", s);
-    if (use_mf) {
-      hipLaunchKernelGGL(k_mf_cands, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax, w.cand_total, w.candE,
-                         w.candF, mp);
-      const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
-      if (same && tuning().score_mf == 2)
-        hipLaunchKernelGGL(k_score_mf2<Src>, dim3(std::max(1, cus)), dim3(kMf2Waves * 64), 0, s, src, pp, bc, cmax,
-                           w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
-      else if (same)
-        hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
-                           w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
-      else
-        hipLaunchKernelGGL((k_score_mf<Src, false>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
-                           w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
-    } else if (prec == 32)
-      hipLaunchKernelGGL((k_score<false, Src, 32>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
-    else if (prec == 16)
-      hipLaunchKernelGGL((k_score<false, Src, 16>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
-    else if (fast32 && same && tuning().score_mfma)
-      hipLaunchKernelGGL(k_score_mx<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
-    else if (fast32)
-      hipLaunchKernelGGL(k_score32<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
-    else if (fast)
-      hipLaunchKernelGGL((k_score<true, Src>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
-    else
-      hipLaunchKernelGGL((k_score<false, Src>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.cntT, w.cntR, kc);
+    score_dispatch(src, pp, bc, cmax, ScoreBufs{w.cand_total, w.candE, w.candF, w.cntT, w.cntR}, kc, mp, use_mf,
+                   same, prec, fast, fast32, cus, grid, s);
   }
   SFM_LAUNCHED();
   {
@@ -1812,6 +1848,74 @@ int sfm_ransac5_flow(const float* flow, int batch, int H, int W, int h_side, int
   const FlowSrc src{flow, Kinv, H, W, w_side - 2 * margin, margin, 1.0 / (double)(w_side - 2 * margin)};
   return run_src(src, n.data(), batch, num_test, num_ransac_test, iters, thr, seed, cheirality, workspace,
                  workspace_bytes, E_out, P_out, inliers_out, winner_out, hyp_score_out, (hipStream_t)stream);
+}
+
+size_t sfm_score_essentials_workspace_bytes(int batch, int ncand) {
+  if (batch < 1 || batch > SFM_MAX_BATCH || ncand < 1) return 0;
+  const size_t c = (size_t)batch * ncand;
+  return align_up(SFM_MAX_BATCH * 4) + align_up(c * kCandStride * 8) + align_up(c * kMfRec * 2) + align_up(c * 4);
+}
+
+int sfm_score_essentials(const double* pts, int64_t n_stride, const int64_t* n, int batch, const double* E,
+                         int ncand, double thr, int32_t* counts, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+  SFM_REQUIRE(pts && n && E && counts, "null pointer argument");
+  SFM_REQUIRE(batch >= 1 && batch <= SFM_MAX_BATCH, "batch must be in [1, 64]");
+  SFM_REQUIRE(ncand >= 1 && ncand <= (1 << 20), "ncand must be in [1, 2^20]");
+  SFM_REQUIRE(thr > 0.0, "inlier threshold must be > 0");
+  SFM_REQUIRE(n_stride >= 1 && n_stride <= (int64_t)INT32_MAX, "n_stride out of range");
+  for (int b = 0; b < batch; ++b) SFM_REQUIRE(n[b] >= 1 && n[b] <= n_stride, "each n[b] must be in [1, n_stride]");
+  const size_t need = sfm_score_essentials_workspace_bytes(batch, ncand);
+  if (!workspace || workspace_bytes < need) {
+    set_error("workspace too small: need " + std::to_string(need) + " bytes");
+    return SFM_ERR_WORKSPACE;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  char* p = (char*)workspace;
+  const size_t c = (size_t)batch * ncand;
+  ScoreBufs w;
+  w.cand_total = (int32_t*)p;
+  p += align_up(SFM_MAX_BATCH * 4);
+  w.candE = (double*)p;
+  p += align_up(c * kCandStride * 8);
+  w.candF = (_Float16*)p;
+  p += align_up(c * kMfRec * 2);
+  w.cntR = (int32_t*)p;
+  w.cntT = counts;
+  PairParams pp{};
+  for (int b = 0; b < batch; ++b) {
+    pp.n[b] = n[b];
+    pp.test[b] = pp.rtest[b] = (int32_t)n[b];
+    pp.splits[b] = (int32_t)((n[b] + kPtsPerItem - 1) / kPtsPerItem);
+  }
+  const int prec = tuning().score_precision;
+  const bool fast = prec == 64 && thr >= 0x1p-40 && thr < 1.0;
+  const double guard_g = fast ? 0x1p24 * (11.0 + 11.0 / thr) : 0.0;
+  const bool fast32 = fast && thr >= 0x1p-20 && tuning().score_fp32;
+  ScoreConsts kc{};
+  kc.thr = thr;
+  kc.t2lo = (thr * thr) * (1.0 - 0x1p-22);
+  kc.t2hi = (thr * thr) * (1.0 + 0x1p-22);
+  kc.t2lo32 = (float)((thr * thr) * (1.0 - 0x1p-6 - 0x1p-19));
+  kc.t2hi32 = (float)((thr * thr) * (1.0 + 0x1p-7) / (1.0 - 0x1p-7) * (1.0 + 0x1p-19));
+  kc.fast32 = fast32 ? 1 : 0;
+  kc.prune = 0;
+  kc.ws_batch = batch;
+  kc.interleave = tuning().score_interleave;
+  MfParams mp{};
+  const bool use_mf = fast32 && tuning().score_mf && !tuning().score_mfma && mf_params(thr, &mp);
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = std::max(1, cus) * tuning().score_blocks_per_cu;
+  SFM_HIP(hipMemsetAsync(w.cntT, 0, c * 4, s));
+  SFM_HIP(hipMemsetAsync(w.cntR, 0, c * 4, s));
+  hipLaunchKernelGGL(k_fill_cands, dim3((ncand + 255) / 256, batch), dim3(256), 0, s, E, ncand, ncand, guard_g, thr,
+                     fast32 ? 1 : 0, w.candE, w.cand_total);
+  ProfScope ps("score_essentials", s);
+  score_dispatch(PackedSrc{pts, n_stride}, pp, batch, ncand, w, kc, mp, use_mf, true, prec, fast, fast32, cus, grid,
+                 s);
+  SFM_LAUNCHED();
+  return SFM_OK;
 }
 
 int sfm_ransac5_inlier_mask(const double* pts, int64_t n_stride, const int64_t* n, int batch, const double* E,

@@ -36,10 +36,14 @@
 #ifndef SFM_MF2_SPAN
 #define SFM_MF2_SPAN 1024
 #endif
-constexpr int kMf2Waves = 12;                  // 3 per SIMD
+#ifndef SFM_MF2_WAVES
+#define SFM_MF2_WAVES 12
+#endif
+constexpr int kMf2Waves = SFM_MF2_WAVES;       // 12: 3 per SIMD, two accumulator sets; 16: 4 per SIMD, one
+constexpr int kMf2Wpe = kMf2Waves / 4;
 constexpr int kMf2Span = SFM_MF2_SPAN;         // points per staged span
 constexpr int kMf2Tiles = kMf2Span / 32;       // tiles per span (every run decides all of them)
-constexpr int kMf2Queue = 512;                 // undecided entries per wave and drain window
+constexpr int kMf2Queue = kMf2Waves > 12 ? 256 : 512;   // undecided entries per wave and drain window (LDS)
 static_assert(kMf2Tiles <= 32 && kMf2Tiles % 2 == 0, "32-bit decision strings, tiles in pairs");
 
 #ifdef SFM_MF_STATS
@@ -92,7 +96,7 @@ __device__ __forceinline__ int mf2_lane() {
 }
 
 template <class Src>
-__global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_score_mf2(
+__global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(kMf2Wpe, kMf2Wpe))) void k_score_mf2(
     const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
     const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
     int32_t* __restrict__ cntR, ScoreConsts kc) {
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     auto claim = [&]() {
       int j = 0;
       if (mf2_lane() == 0) j = atomicAdd(&s_claim, 1);
-      return k0 + __builtin_amdgcn_readfirstlane(__shfl(j, 0, 64));
+      return k0 + __builtin_amdgcn_readfirstlane(j);      // lane 0 is the first active lane
     };
     int k = claim();
     if (k < k1) load_rows(b, k);
@@ -208,6 +212,18 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
       for (int g = 0; g < 16; ++g) { s1[g] = 0u; s2[g] = 0u; }
       {
+#if SFM_MF2_WAVES > 12
+        // four waves per SIMD (128 VGPRs): one accumulator set, the B
+        // fragments one tile ahead; the other waves cover the MFMA latency
+        MfB bn = mf_load_b(fr, mf2_lane());
+#pragma unroll 1
+        for (int t = 0; t < kMf2Tiles; ++t) {
+          const MfB bc = bn;
+          if (t + 1 < kMf2Tiles) bn = mf_load_b(fr + (size_t)(t + 1) * kTileHalves, mf2_lane());
+          const MfAcc r = mf_tile_mfma(bc, A1, A2, AL, AH);
+          mf2_decide(r, s1, s2);
+        }
+#else
         // two accumulator sets: tile t+1's MFMAs beside tile t's decisions
         // (the last pair peeled, so the loop body has no conditional MFMA)
         MfB B = mf_load_b(fr, mf2_lane());
@@ -225,6 +241,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         rb = mf_tile_mfma(B, A1, A2, AL, AH);
         mf2_decide(ra, s1, s2);
         mf2_decide(rb, s1, s2);
+#endif
       }
       MF_STAMP(1);
       const int lane = mf2_lane(), hl = lane >> 5, rl = lane & 31;

@@ -84,6 +84,10 @@ _SIGS = [
       ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
     ("sfm_to_channels_last_f32", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp]),
+    ("sfm_score_essentials_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),
+    ("sfm_score_essentials", ctypes.c_int,
+     [_c_dp, ctypes.c_int64, _i64p, ctypes.c_int, _c_dp, ctypes.c_int, ctypes.c_double, _c_dp, _c_dp,
+      ctypes.c_size_t, _c_dp]),
     ("sfm_tune_set", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("sfm_tune_get", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     ("sfm_profile_enable", ctypes.c_int, [ctypes.c_int]),

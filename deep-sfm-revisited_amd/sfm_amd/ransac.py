@@ -147,6 +147,25 @@ def ransac5_batched(pts, n=None, num_test_points=None, num_ransac_test_points=No
     return out + (scores,) if return_scores else out
 
 
+def score_essentials(pts, E, threshold, n=None):
+    """Exact inlier counts of given essential matrices (the reference's
+    ComputeError test, e <= thr) through the RANSAC's own scorer: pts [B, N, 4]
+    float64, E [B, C, 3, 3] (or [B, C, 9]) float64 -> counts [B, C] int32."""
+    _check_dev_f64(pts, "pts")
+    B, ns, _ = pts.shape
+    n = [ns] * B if n is None else [int(v) for v in n]
+    E = E.reshape(B, -1, 9).to(pts.device, torch.float64).contiguous()
+    C = E.shape[1]
+    L = _lib.load()
+    counts = torch.empty(B, C, dtype=torch.int32, device=pts.device)
+    with torch.cuda.device(pts.device):
+        ws = torch.empty(int(L.sfm_score_essentials_workspace_bytes(B, C)), dtype=torch.uint8, device=pts.device)
+        _lib.check(L.sfm_score_essentials(_lib.ptr(pts), ns, _lib.i64_array(n), B, _lib.ptr(E), C, float(threshold),
+                                          _lib.ptr(counts), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(pts.device)),
+                   "sfm_score_essentials")
+    return counts
+
+
 def workspace_for(batch, iters, device):
     """Pre-allocate a reusable workspace for ransac5_batched (graph capture)."""
     return _workspace(batch, 0, iters, device)

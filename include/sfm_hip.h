@@ -112,6 +112,22 @@ int sfm_ransac5_flow(const float* flow, int batch, int H, int W, int h_side, int
                      double* E_out, double* P_out, int32_t* inliers_out, int32_t* winner_out,
                      int32_t* hyp_score_out, void* stream);
 
+/* Inlier counts of given essential matrices over packed correspondences:
+ * counts[b][c] = #{k < n[b] : e(E[b][c], point k) <= thr} with e the
+ * reference's ComputeError<double> Sampson-style error
+ * (kernel_functions.cu:232-264), through the same scorer the RANSAC uses
+ * (split-f16 matrix-core decisions exact by bound + float64 re-test; the
+ * float32 / float64 VALU scorers outside its threshold range), bit-exact.
+ * The reference's scoring loop over a candidate set (kernel_functions.cu:
+ * 187-214) without the sampling.
+ *   pts [dev] batch x n_stride x 4 float64; n [host] batch;
+ *   E [dev] batch x ncand x 9 float64; counts [dev] batch x ncand int32;
+ *   workspace [dev] sfm_score_essentials_workspace_bytes(batch, ncand). */
+size_t sfm_score_essentials_workspace_bytes(int batch, int ncand);
+int sfm_score_essentials(const double* pts, int64_t n_stride, const int64_t* n, int batch, const double* E,
+                         int ncand, double thr, int32_t* counts, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
 /* Exact inlier mask of E (reference ComputeError + `<= thr`) for each point.
  *   pts [dev] batch x n_stride x 4; n [host] batch; E [dev] batch x 9;
  *   mask [dev] batch x n_stride uint8 (entries >= n[b] are written 0). */
