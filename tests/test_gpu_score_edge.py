@@ -15,7 +15,8 @@ of x along its normal until the reference-order float64 error is
 Each class of points is its own pair of the batch, so a count equals the
 oracle's (the exact float64 reference order, oracle/ransac5_oracle.cpp) only
 if every single decision does (the classes are one-sided).  Thresholds span
-the matrix-core range 2^-15 .. 0.3 plus one outside it (VALU scorer)."""
+the matrix-core range 2^-15 .. 0.3, plus 1e-6 below it (the float32 VALU
+scorer k_score32)."""
 import numpy as np
 import pytest
 import torch
@@ -66,12 +67,22 @@ def _offsets(E, q, target):
     lo = np.zeros(len(q))
     hi = np.full(len(q), 0.05)
     f = lambda s: _err(E, q, base + s[:, None] * nrm)
-    for _ in range(60):                         # widen until every point's bracket holds the crossing
+    for _ in range(40):                         # widen until every point's bracket holds the crossing
         up = f(hi) <= target
         if not up.any():
             break
         hi = np.where(up, 2 * hi, hi)
-    assert (f(hi) > target).all()
+    # far from the line the error saturates (a and x'^T E both grow with the
+    # offset): at large thresholds some points never cross; they take a
+    # crossing point's offset instead (the set stays one-sided per class)
+    ok = f(hi) > target
+    assert ok.sum() >= len(q) // 4
+    src = np.flatnonzero(ok)
+    fill = src[np.arange(len(q)) % len(src)]
+    q[:] = np.where(ok[:, None], q, q[fill])
+    base = np.where(ok[:, None], base, base[fill])
+    nrm = np.where(ok[:, None], nrm, nrm[fill])
+    hi = np.where(ok, hi, hi[fill])
     for _ in range(200):
         mid = 0.5 * (lo + hi)
         up = f(mid) > target
@@ -80,7 +91,7 @@ def _offsets(E, q, target):
     return base, nrm, lo, hi
 
 
-@pytest.mark.parametrize("thr", [2.0 ** -15, 1e-4, 1e-3, 0.3, 2.0])
+@pytest.mark.parametrize("thr", [1e-6, 2.0 ** -15, 1e-4, 1e-3, 0.3])
 def test_decisions_at_the_threshold_and_band_edges(cuda, thr):
     from sfm_amd import ransac
     rng = np.random.default_rng(int(thr * 1e6) + 3)
@@ -91,6 +102,7 @@ def test_decisions_at_the_threshold_and_band_edges(cuda, thr):
     per_e = []
     for E in Es:
         q = rng.uniform(-0.6, 0.6, (n_p, 2))
+        _offsets(E, q, thr * (1 + rels[-1]))   # the largest target first: fixes q (smaller targets all cross)
         base, nrm, lo, hi = _offsets(E, q, thr)
         pts = {"edge_in": base + lo[:, None] * nrm, "edge_out": base + hi[:, None] * nrm}
         for r in rels:
