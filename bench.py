@@ -122,7 +122,41 @@ def pmc_traffic(args):
     return {}, None
 
 
-def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, traffic_src):
+def _stats_version(path):
+    """profiles/r03_kernel_stats_v4.csv -> (3, 4); a config tag (r03_kernel_stats_c3_v1.csv) is allowed."""
+    m = re.search(r"r(\d+)_kernel_stats(?:_(?!v\d)([a-z0-9]+))?(?:_v(\d+))?\.csv$", os.path.basename(path))
+    if not m:
+        return None
+    tag = m.group(2) or "c2"
+    return tag, (int(m.group(1)), int(m.group(3) or 0))
+
+
+def rocprof_kernel_ms(args, prefixes):
+    """Average launch duration (ms) of the kernels named by ``prefixes`` (summed:
+    one launch each per step) from the newest committed rocprofv3 --stats
+    summary of this workload (profiles/rNN_kernel_stats[_cfg]_vK.csv, written
+    by scripts/gpu_profile.sh from a profiled run of this bench), so the line
+    carries a frac that follows from the committed profile, beside the live
+    HIP-event one."""
+    import csv
+    import glob
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats*.csv")):
+        v = _stats_version(f)
+        if v and v[0] == args.config and (best is None or v[1] > best[0]):
+            best = (v[1], f)
+    if best is None:
+        return None, None
+    tot, hit = 0.0, False
+    with open(best[1]) as fh:
+        for row in csv.DictReader(fh):
+            if any(p in row["Name"] for p in prefixes):
+                tot += float(row["AverageNs"]) * 1e-6
+                hit = True
+    return (tot if hit else None), os.path.relpath(best[1], ROOT)
+
+
+def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, traffic_src, rocprof=None):
     """Roofline line of the RANSAC scoring kernel.  achieved = the algorithmic
     rate (SURVEY §8d: 50 FLOP per (candidate E, correspondence) evaluation);
     peak = the unit that executes it: the dense f16 MFMA peak for k_score_mf
@@ -133,11 +167,19 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
             f"minus {skipped} skipped by exact bound pruning ({100.0 * skipped / max(evals, 1):.1f}%)")
     if use_mf:
         issued = evals * MF_MFMA_FLOP_PER_EVAL / (ms * 1e-3) / 1e12
-        return {"kernel": "ransac_score (k_score_mf)", "bound": "mfma-f16", "achieved": round(tflops, 3),
+        rp = None
+        if rocprof and rocprof[0]:
+            t = done * FLOP_PER_EVAL / (rocprof[0] * 1e-3) / 1e12
+            rp = {"avg_launch_ms": round(rocprof[0], 4), "achieved": round(t, 3),
+                  "frac": round(t / PEAK_F16_TFLOPS, 4), "source": rocprof[1],
+                  "note": "k_mf_cands + k_score_mf2 averages of the committed rocprofv3 --stats summary of this "
+                          "workload (a profiled run clocks lower than this one)"}
+        return {"kernel": "ransac_score (k_mf_cands + k_score_mf2)", "bound": "mfma-f16", "achieved": round(tflops, 3),
                 "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_F16_TFLOPS, 4),
                 "mfma_issued": {"flop_per_eval": MF_MFMA_FLOP_PER_EVAL, "tflops": round(issued, 1),
                                 "frac": round(issued / PEAK_F16_TFLOPS, 4)},
-                "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work}
+                "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work,
+                "rocprof": rp}
     return {"kernel": "ransac_score (k_score32)", "bound": "valu-fp32", "achieved": round(tflops, 3),
             "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work}
@@ -399,7 +441,8 @@ def _main_gpu(args, dist):
                      "backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
                      "devices": names},
             "roofline": score_roofline(use_mf, score_tflops, done, evals, skipped, sum(cands), hp.n, score_ms,
-                                       traffic.get("ransac_score"), traffic_src),
+                                       traffic.get("ransac_score"), traffic_src,
+                                       rocprof_kernel_ms(args, ("k_score_mf2", "k_mf_cands"))),
             "roofline_sweep": {"kernel": "plane_sweep", "bound": "hbm", "achieved": round(sweep_gbs, 1),
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(sweep_gbs / PEAK_HBM_GBS, 4),
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,

@@ -33,6 +33,9 @@
 #ifndef SFM_MF2_SCHED
 #define SFM_MF2_SCHED 1
 #endif
+#ifndef SFM_MF2_EARLY_CLAIM
+#define SFM_MF2_EARLY_CLAIM 0
+#endif
 #ifndef SFM_MF2_SPAN
 #define SFM_MF2_SPAN 1024
 #endif
@@ -147,11 +150,11 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   unsigned long long mf_acc_[kMfStamps] = {};
 #endif
   // A rows of candidate tile k of pair b (absent rows: every evaluation a decided outlier)
-  auto load_rows = [&](int bb, int k) {
+  auto load_rows = [&](int bb, int k, int ctot) {
     const int ln = mf2_lane();
     const int lh = ln >> 5, lr = ln & 31;
     const int c = k * kKC + lr;
-    if (c < s_ctot[bb]) {
+    if (c < ctot) {
       const mf_half8* rec = reinterpret_cast<const mf_half8*>(candF + ((size_t)bb * cmax + c) * kMfRec);
       A1 = rec[0 + lh];
       A2 = rec[2 + lh];
@@ -201,7 +204,8 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       return k0 + __builtin_amdgcn_readfirstlane(j);      // lane 0 is the first active lane
     };
     int k = claim();
-    if (k < k1) load_rows(b, k);
+    const int ctot = __builtin_amdgcn_readfirstlane(s_ctot[b]);   // the pair's candidates, in an SGPR
+    if (k < k1) load_rows(b, k, ctot);
 #pragma unroll 1
     while (k < k1) {
 #ifdef SFM_MF_STAMPS
@@ -211,6 +215,11 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       uint32_t s1[16], s2[16];
 #pragma unroll
       for (int g = 0; g < 16; ++g) { s1[g] = 0u; s2[g] = 0u; }
+#if SFM_MF2_EARLY_CLAIM
+      // the next run's claim flies during this run's tile loop
+      int jn = 0;
+      if (mf2_lane() == 0) jn = atomicAdd(&s_claim, 1);
+#endif
       {
 #if SFM_MF2_WAVES > 12
         // four waves per SIMD (128 VGPRs): one accumulator set, the B
@@ -246,8 +255,12 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       MF_STAMP(1);
       const int lane = mf2_lane(), hl = lane >> 5, rl = lane & 31;
       // the next run's rows load under this run's queue, drain and reduction
+#if SFM_MF2_EARLY_CLAIM
+      const int kn = k0 + __builtin_amdgcn_readfirstlane(jn);
+#else
       const int kn = claim();
-      if (kn < k1) load_rows(b, kn);
+#endif
+      if (kn < k1) load_rows(b, kn, ctot);
       MF_STAMP(6);
       // 3. undecided evaluations -> the queue -> float64.  Bit j of a string
       // is tile kMf2Tiles-1-j, point 32 (kMf2Tiles-1-j) + rl of the span.
@@ -304,7 +317,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         const int c = mf_row((rl >> 1) & 15, hl);
         const int d = sumT + cnt[c];
         cnt[c] = 0;
-        if (d && c0 + c < s_ctot[b]) {
+        if (d && c0 + c < ctot) {
           atomicAdd(cntT + (size_t)b * cmax + c0 + c, d);
           atomicAdd(cntR + (size_t)b * cmax + c0 + c, d);
         }

@@ -85,3 +85,12 @@ def test_pmc_traffic_matches_the_workload():
     assert src4 and "_c4" in src4
     # same config, a batch no summary was collected on
     assert bench.pmc_traffic(args("c2", batch=3)) == ({}, None)
+
+
+def test_kernel_stats_files_sort_numerically():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench._stats_version("profiles/r03_kernel_stats_v10.csv") == ("c2", (3, 10))
+    assert bench._stats_version("profiles/r03_kernel_stats_v9.csv") < bench._stats_version("profiles/r03_kernel_stats_v10.csv")
+    assert bench._stats_version("profiles/r02_kernel_stats_sparse_v3.csv") == ("sparse", (2, 3))
+    assert bench._stats_version("profiles/r01_regularize_kernel_stats.csv") is None
