@@ -147,13 +147,17 @@ def rocprof_kernel_ms(args, prefixes):
             best = (v[1], f)
     if best is None:
         return None, None
-    tot, hit = 0.0, False
+    tot, hit = 0.0, set()
     with open(best[1]) as fh:
         for row in csv.DictReader(fh):
-            if any(p in row["Name"] for p in prefixes):
-                tot += float(row["AverageNs"]) * 1e-6
-                hit = True
-    return (tot if hit else None), os.path.relpath(best[1], ROOT)
+            for p in prefixes:
+                # mangled names: the prefix must be followed by a non-identifier character
+                if re.search(re.escape(p) + r"(?![A-Za-z0-9_])", row["Name"]):
+                    tot += float(row["AverageNs"]) * 1e-6
+                    hit.add(p)
+                    break
+    # every named kernel must be in the summary (an older scorer's profile does not count)
+    return (tot if hit == set(prefixes) else None), os.path.relpath(best[1], ROOT)
 
 
 def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, traffic_src, rocprof=None):
