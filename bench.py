@@ -151,8 +151,8 @@ def rocprof_kernel_ms(args, prefixes):
     with open(best[1]) as fh:
         for row in csv.DictReader(fh):
             for p in prefixes:
-                # mangled names: the prefix must be followed by a non-identifier character
-                if re.search(re.escape(p) + r"(?![A-Za-z0-9_])", row["Name"]):
+                # whole kernel names: mangled (length-prefixed, "11k_score_mf2") or demangled
+                if f"{len(p)}{p}" in row["Name"] or re.search(r"\b" + re.escape(p) + r"[<(]", row["Name"]):
                     tot += float(row["AverageNs"]) * 1e-6
                     hit.add(p)
                     break

@@ -94,3 +94,22 @@ def test_kernel_stats_files_sort_numerically():
     assert bench._stats_version("profiles/r03_kernel_stats_v9.csv") < bench._stats_version("profiles/r03_kernel_stats_v10.csv")
     assert bench._stats_version("profiles/r02_kernel_stats_sparse_v3.csv") == ("sparse", (2, 3))
     assert bench._stats_version("profiles/r01_regularize_kernel_stats.csv") is None
+
+
+def test_rocprof_kernel_match_is_whole_name(tmp_path, monkeypatch):
+    """k_score_mf must not match k_score_mf2's row (or the reverse): the
+    rocprof frac is only reported from a summary holding every named kernel."""
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r09_kernel_stats_v1.csv").write_text(
+        '"Name","Calls","TotalDurationNs","AverageNs"\n'
+        '"_ZN3sfm11k_score_mf2INS_9PackedSrcEEEvT_",2,10000000,5000000\n'
+        '"_ZN3sfm10k_mf_candsEiPKi",2,20000,10000\n')
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+
+    class A:
+        config = "c2"
+    ms, src = bench.rocprof_kernel_ms(A, ("k_score_mf2", "k_mf_cands"))
+    assert abs(ms - 5.01) < 1e-9 and src.endswith("r09_kernel_stats_v1.csv")
+    assert bench.rocprof_kernel_ms(A, ("k_score_mf", "k_mf_cands"))[0] is None
