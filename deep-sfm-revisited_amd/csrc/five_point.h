@@ -871,6 +871,255 @@ __device__ __forceinline__ void isolate_r(const SturmR& S, double lo, double hi,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split isolation (k_roots_split, tuning key roots_split = 1, default).
+//
+// isolate_r above advances each lane through pops, bisections and
+// regula-falsi steps in one loop, so every pass pays for all three whenever
+// any lane of the wave is in each mode, and a wave lasts as long as its
+// busiest hypothesis (p50 11 Sturm evaluations + 38 falsi steps, p99 89 + 70:
+// scripts/roots_stats.py).  The falsi refinement of an isolated single-root
+// interval depends on nothing but the interval and the polynomial, and its
+// root lands at a fixed slot (ioff), so the work is split in phases:
+//   1. each hypothesis lane runs the isolation with the bisections and
+//      modrf's case analysis and end-point evaluations, but where isolate_r
+//      would enter the falsi loop it appends a task (a, b, f(a), f(b), the
+//      interval, its slot) to the wave's task list in LDS;
+//   2. all 64 lanes of the wave then run the falsi loop over the task list,
+//      each lane claiming the next task when its own ends (a ballot and a
+//      prefix count, no atomics): one kind of step per pass, and the ~77
+//      tasks of a 32-hypothesis wave spread over 64 lanes;
+//   3. a task whose falsi loop gives up (modrf_pos's iteration limit: the
+//      reference then bisects the interval with the Sturm sequence) goes
+//      back to its hypothesis lane, which holds the sequence in registers.
+// Every interval sees exactly the reference's operations in their order, and
+// roots are written to their slot, so the roots are bit-identical to
+// isolate_r's (tests/test_gpu_ransac.py, test_gpu_solve.py: solve5.npz).
+// ---------------------------------------------------------------------------
+constexpr int kRootTasks = kStkLanes * 10;   // a hypothesis has at most 10 isolated roots
+constexpr int kTaskDefer = 1 << 20;          // tmeta flag: falsi gave up, bisect on the owner lane
+struct RootsShared {                         // one wave's LDS (k_roots_split: one wave per block)
+  double ta[kRootTasks], tb[kRootTasks], tfa[kRootTasks], tfb[kRootTasks];   // falsi start
+  double tmn[kRootTasks], tmx[kRootTasks];   // the node's interval (the bisection fallback)
+  int tmeta[kRootTasks];                     // owner lane | ioff << 8 | inv << 16 | kTaskDefer
+  int tatlo[kRootTasks];                     // sign changes at the node's low end
+  double poly[11][kStkLanes];                // each hypothesis' s[0]
+  double roots[10][kStkLanes];               // root slots (scaled), 0 where none is found
+  int ntask, ndefer;
+};
+
+// phase 1: isolate_r with the falsi loop replaced by a task append
+__device__ __forceinline__ void isolate_p1(const SturmR& S, double lo, double hi, int atlo, int athi,
+                                           const IsoStack& stk, RootsShared& sh, int lane) {
+  constexpr int kPop = 0, kBis1 = 2, kBisN = 3;
+  const double* c = S.c;
+  int sp = 0;
+  stk.put(sp++, lo, hi, atlo, athi, 0, 0);
+  int mode = kPop, it = 0;
+  int iatlo = 0, iathi = 0, ioff = 0, idepth = 0;
+  double mn = 0.0, mx = 0.0, mid = 0.0;
+  for (;;) {
+    if (mode == kPop) {
+      if (sp == 0) break;
+      --sp;
+      mn = stk.lohi[(2 * sp) * kStkLanes];
+      mx = stk.lohi[(2 * sp + 1) * kStkLanes];
+      iatlo = stk.ints[(4 * sp) * kStkLanes];
+      iathi = stk.ints[(4 * sp + 1) * kStkLanes];
+      ioff = stk.ints[(4 * sp + 2) * kStkLanes];
+      idepth = stk.ints[(4 * sp + 3) * kStkLanes];
+      if (idepth >= kMaxDepth) continue;
+      it = 0;
+      if (iatlo - iathi != 1) {
+        mode = kBisN;
+      } else {
+        double a = mn, b = mx, fa, fb;
+        bool inv;
+        if (a > b) { const double t = a; a = b; b = t; }
+        if (b <= 1.0 && a >= -1.0) {
+          inv = false;
+        } else if (a >= 1.0 || b <= -1.0) {
+          inv = true;
+        } else {
+          double fp1 = 0.0, fm1 = 0.0, ga = 0.0, gb = 0.0;
+#pragma unroll
+          for (int i = 9; i >= 0; --i) {
+            fp1 = c[i] + fp1;
+            fm1 = c[i] - fm1;
+            ga = a * ga + c[i];
+            gb = b * gb + c[i];
+          }
+          if (a < -1.0 && b > 1.0) {
+            if (ga * fm1 < 0.0) { b = -1.0; inv = true; }
+            else if (gb * fp1 < 0.0) { a = 1.0; inv = true; }
+            else { a = -1.0; b = 1.0; inv = false; }
+          } else if (a < -1.0) {
+            if (ga * fm1 < 0.0) { b = -1.0; inv = true; }
+            else { a = -1.0; inv = false; }
+          } else {
+            if (gb * fp1 < 0.0) { a = 1.0; inv = true; }
+            else { b = 1.0; inv = false; }
+          }
+        }
+        if (inv) { const double t = a; a = 1.0 / b; b = 1.0 / t; }
+        if (inv) {
+          fa = fb = c[0];
+#pragma unroll
+          for (int i = 1; i <= 10; ++i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
+        } else {
+          fa = fb = c[10];
+#pragma unroll
+          for (int i = 9; i >= 0; --i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
+        }
+        if (fa * fb > 0.0) {
+          mode = kBis1;                                        // modrf failed: bisection on [mn, mx]
+        } else if (fabs(fa) < kRelErr) {
+          sh.roots[ioff][lane] = inv ? 1.0 / a : a;           // stays kPop
+        } else if (fabs(fb) < kRelErr) {
+          sh.roots[ioff][lane] = inv ? 1.0 / b : b;
+        } else {
+          const int t = atomicAdd(&sh.ntask, 1);               // the falsi loop: phase 2
+          sh.ta[t] = a;
+          sh.tb[t] = b;
+          sh.tfa[t] = fa;
+          sh.tfb[t] = fb;
+          sh.tmn[t] = mn;
+          sh.tmx[t] = mx;
+          sh.tmeta[t] = lane | (ioff << 8) | (inv ? 1 << 16 : 0);
+          sh.tatlo[t] = iatlo;
+        }
+      }
+    }
+    if (mode >= kBis1) {
+      mid = (double)((mn + mx) / 2);
+      bool stop = false;
+      if (mode == kBis1) {
+        if (fabs(mid) > kRelErr) stop = fabs((mx - mn) / mid) < kRelErr;
+        else stop = fabs(mx - mn) < kRelErr;
+      }
+      if (!stop) {
+        const int atmid = sign_changes_r(S, mid);
+        if (mode == kBis1) {
+          if ((iatlo - atmid) == 0) mn = mid; else mx = mid;
+          stop = ++it == kMaxIt;
+        } else {
+          const int n1 = iatlo - atmid, n2 = atmid - iathi;
+          if (n1 != 0 && n2 != 0) {
+            if (sp + 2 <= kStkDepth) {
+              stk.put(sp++, mid, mx, atmid, iathi, ioff + n1, idepth + 1);
+              stk.put(sp++, mn, mid, iatlo, atmid, ioff, idepth + 1);
+            }
+            mode = kPop;
+          } else {
+            const bool fixed = (n1 == 0) ? mid == mn : mid == mx;
+            if (n1 == 0) mn = mid; else mx = mid;
+            if (fixed) it = kMaxIt - 1;
+            if (++it == kMaxIt) {
+              for (int r = iathi; r < iatlo; ++r) sh.roots[ioff + r - iathi][lane] = mid;
+              mode = kPop;
+            }
+          }
+        }
+      }
+      if (stop) { sh.roots[ioff][lane] = mid; mode = kPop; }
+    }
+  }
+}
+
+// phase 2: modrf_pos's loop (sturm.cu:82-205) over the wave's task list, on every lane
+__device__ __forceinline__ void falsi_tasks(RootsShared& sh, int lane) {
+  const int ntask = sh.ntask;
+  int next = 0, cur = -1, it = 0, owner = 0, ioff = 0;
+  bool inv = false;
+  double a = 0.0, b = 0.0, fa = 0.0, fb = 0.0, lfx = 0.0;
+  double c[11];
+#pragma unroll
+  for (int i = 0; i <= 10; ++i) c[i] = 0.0;
+  for (;;) {
+    const unsigned long long idle = __ballot(cur < 0);
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(idle >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)idle, 0u));
+    if (cur < 0 && next + rank < ntask) {
+      cur = next + rank;
+      a = sh.ta[cur];
+      b = sh.tb[cur];
+      fa = sh.tfa[cur];
+      fb = sh.tfb[cur];
+      lfx = fa;
+      const int m = sh.tmeta[cur];
+      owner = m & 0xff;
+      ioff = (m >> 8) & 0xff;
+      inv = (m >> 16) & 1;
+      it = 0;
+#pragma unroll
+      for (int i = 0; i <= 10; ++i) c[i] = sh.poly[i][owner];
+    }
+    next += __popcll(idle);
+    if (__ballot(cur >= 0) == 0ull) break;
+    if (cur >= 0) {
+      ROOTS_COUNT(g_roots_falsi);
+      const double x = (fb * a - fa * b) / (fb - fa);
+      double fx;
+      if (inv) {
+        fx = c[0];
+#pragma unroll
+        for (int i = 1; i <= 10; ++i) fx = x * fx + c[i];
+      } else {
+        fx = c[10];
+#pragma unroll
+        for (int i = 9; i >= 0; --i) fx = x * fx + c[i];
+      }
+      bool found = false;
+      double v = x;
+      if (fabs(x) > kRelErr && fabs(fx / x) < kRelErr) found = true;
+      else if (fabs(fx) < kRelErr) found = true;
+      if (!found) {
+        if ((fa * fx) < 0) { b = x; fb = fx; if ((lfx * fx) > 0) fa /= 2; }
+        else { a = x; fa = fx; if ((lfx * fx) > 0) fb /= 2; }
+        if (fabs(b - a) < fabs(kRelErr * a)) {
+          found = true;
+          v = a;
+        } else {
+          lfx = fx;
+          if (++it == kMaxIt) {                                // modrf_pos gave up: phase 3
+            sh.tmeta[cur] |= kTaskDefer;
+            sh.ndefer = 1;
+            cur = -1;
+          }
+        }
+      }
+      if (found) {
+        sh.roots[ioff][owner] = inv ? 1.0 / v : v;
+        cur = -1;
+      }
+    }
+  }
+}
+
+// phase 3: sbisect's bisection after a failed modrf, on the owner lane (sturm.cu:465-497)
+__device__ __forceinline__ void bisect_deferred(const SturmR& S, RootsShared& sh, int lane) {
+  const int ntask = sh.ntask;
+  for (int t = 0; t < ntask; ++t) {
+    const int m = sh.tmeta[t];
+    if (!(m & kTaskDefer) || (m & 0xff) != lane) continue;
+    double mn = sh.tmn[t], mx = sh.tmx[t], mid;
+    const int iatlo = sh.tatlo[t];
+    int it = 0;
+    for (;;) {
+      mid = (double)((mn + mx) / 2);
+      bool stop;
+      if (fabs(mid) > kRelErr) stop = fabs((mx - mn) / mid) < kRelErr;
+      else stop = fabs(mx - mn) < kRelErr;
+      if (!stop) {
+        const int atmid = sign_changes_r(S, mid);
+        if ((iatlo - atmid) == 0) mn = mid; else mx = mid;
+        stop = ++it == kMaxIt;
+      }
+      if (stop) break;
+    }
+    sh.roots[(m >> 8) & 0xff][lane] = mid;
+  }
+}
+
 // buildsturm + modp (sturm.cu:285-360) on registers, for the generic case in
 // which every remainder keeps its full degree (ord[k] = 10 - k: no leading
 // coefficient falls under kSmall before the last step).  The operations are
@@ -938,9 +1187,13 @@ __device__ __forceinline__ int count_real_roots_r(const SturmR& R, int* atneg, i
 }
 
 // find_real_roots_sturm (sturm.cu:557-676) with the iterative part on the
-// register-resident sequence; identical results to real_roots.
-__device__ __forceinline__ int real_roots_r(const double poly[11], double roots[10], const IsoStack& stk) {
-  SturmR R;
+// register-resident sequence; identical results to real_roots.  SPLIT: phase 1
+// of the split isolation (isolate_p1; the roots are completed by phases 2-3
+// in sh and scaled by the caller with *fac_out); R is left holding the
+// sequence for phase 3.
+template <bool SPLIT>
+__device__ __forceinline__ int real_roots_t(const double poly[11], double roots[10], const IsoStack& stk, SturmR& R,
+                                            RootsShared* sh, int lane, double* fac_out) {
 #ifdef SFM_ROOTS_STATS
   unsigned long long ts = __builtin_amdgcn_s_memtime();
 #endif
@@ -990,8 +1243,15 @@ __device__ __forceinline__ int real_roots_r(const double poly[11], double roots[
     nr = atmin - atmax;
     ROOTS_PHASE(2, ts);
     if (nr <= 0) return nr;
-    isolate_r(R, mn, mx, atmin, atmax, roots, stk);
-    for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
+    if constexpr (SPLIT) {
+      *fac_out = fac;
+#pragma unroll
+      for (int i = 0; i <= 10; ++i) sh->poly[i][lane] = R.c[i];
+      isolate_p1(R, mn, mx, atmin, atmax, stk, *sh, lane);
+    } else {
+      isolate_r(R, mn, mx, atmin, atmax, roots, stk);
+      for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
+    }
     ROOTS_PHASE(3, ts);
     return nr;
   }
@@ -1029,10 +1289,22 @@ __device__ __forceinline__ int real_roots_r(const double poly[11], double roots[
     if (nch != atmax) atmax = nch;
     nr = atmin - atmax;
     if (nr <= 0) return nr;
-    isolate_r(R, mn, mx, atmin, atmax, roots, stk);
-    for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
+    if constexpr (SPLIT) {
+      *fac_out = fac;
+#pragma unroll
+      for (int i = 0; i <= 10; ++i) sh->poly[i][lane] = R.c[i];
+      isolate_p1(R, mn, mx, atmin, atmax, stk, *sh, lane);
+    } else {
+      isolate_r(R, mn, mx, atmin, atmax, roots, stk);
+      for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
+    }
     return nr;
   }
+}
+
+__device__ __forceinline__ int real_roots_r(const double poly[11], double roots[10], const IsoStack& stk) {
+  SturmR R;
+  return real_roots_t<false>(poly, roots, stk, R, nullptr, 0, nullptr);
 }
 
 // null_space_solve_3x3_half_pivot (essential_matrix_5pt.cu:476-507)

@@ -1657,6 +1657,63 @@ __global__ __launch_bounds__(256) void k_fill_cands(const double* __restrict__ E
   fp32_constants(dst, thr, fast32 != 0, reinterpret_cast<float*>(dst + 10));
 }
 
+// k_roots with the split isolation (five_point.h, isolate_p1 / falsi_tasks /
+// bisect_deferred): lanes [0, lanes) own one hypothesis each through phase 1
+// and 3; all 64 lanes share the wave's falsi tasks in phase 2.  One wave per
+// block, so the block barriers are wave barriers.
+__global__ __launch_bounds__(64) void k_roots_split(int H, int lanes, double* __restrict__ st, size_t stride,
+                                                    int32_t* __restrict__ out_nroots) {
+  const int b = blockIdx.y;
+  const int lane = (int)threadIdx.x;
+  const int h = blockIdx.x * lanes + lane;
+  const bool own = lane < lanes && h < H;
+  __shared__ double s_lohi[kStkDepth * 2 * kStkLanes];
+  __shared__ int s_ints[kStkDepth * 4 * kStkLanes];
+  __shared__ RootsShared sh;
+  if (lane < kStkLanes) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) sh.roots[i][lane] = 0.0;
+  }
+  if (lane == 0) { sh.ntask = 0; sh.ndefer = 0; }
+  __syncthreads();
+#ifdef SFM_ROOTS_STATS
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+  const size_t hb = (size_t)b * H + h;
+  SturmR R;
+  int nr = 0;
+  double fac = 1.0;
+  if (own) {
+    double poly[11];
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) poly[i] = st_at(st, stride, kStPoly + i, hb);
+    double roots[10];
+    const IsoStack stk{s_lohi + lane, s_ints + lane};
+    nr = real_roots_t<true>(poly, roots, stk, R, &sh, lane, &fac);
+  }
+  __syncthreads();
+  falsi_tasks(sh, lane);
+  __syncthreads();
+  if (sh.ndefer) {
+    if (own) bisect_deferred(R, sh, lane);
+    __syncthreads();
+  }
+  if (own) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      double r = sh.roots[i][lane];
+      if (i < nr) r /= fac;
+      st_at(st, stride, kStRoots + i, hb) = r;
+    }
+    out_nroots[hb] = nr;
+  }
+#ifdef SFM_ROOTS_STATS
+  if (own)
+    g_roots_cycles[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x] =
+        __builtin_amdgcn_s_memtime() - t0;
+#endif
+}
+
 template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
@@ -1680,8 +1737,12 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     const size_t stride = (size_t)bc * H;
     hipLaunchKernelGGL(k_solve_front<Src>, dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H, seed,
                        lanes, w.sstate, stride);
-    hipLaunchKernelGGL(k_roots, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate, stride,
-                       w.nroots);
+    if (tuning().roots_split)
+      hipLaunchKernelGGL(k_roots_split, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate,
+                         stride, w.nroots);
+    else
+      hipLaunchKernelGGL(k_roots, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate, stride,
+                         w.nroots);
     hipLaunchKernelGGL(k_solve_back, dim3((H + 63) / 64, bc), dim3(64), 0, s, H, cheir, w.sstate, stride, w.nroots,
                        w.ncand, w.hypE, w.hypP);
   }

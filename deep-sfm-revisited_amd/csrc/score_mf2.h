@@ -111,8 +111,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   __shared__ int32_t s_tiles[SFM_MAX_BATCH];                 // candidate tiles per pair
   __shared__ int32_t s_ctot[SFM_MAX_BATCH];
   __shared__ int32_t s_claim;                                // next candidate tile of the span to claim
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int hl = lane >> 5, rl = lane & 31;
+  const int tid = threadIdx.x, wv = tid >> 6;
   if (tid == 0) {
     long long acc = 0;
     for (int b = 0; b < batch; ++b) {

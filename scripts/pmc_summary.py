@@ -22,6 +22,16 @@ KERNELS = {"k_sweep_flat": "plane_sweep", "k_score32": "ransac_score", "k_score"
            "k_chain": "ransac_chain", "k_cand": "ransac_chain", "k_tgt_quads": "sweep_tgt_quads", "k_flow_points": "flow_to_points"}
 
 
+def short_name(name):
+    """k_score_mf2 from a mangled or demangled kernel name."""
+    import re
+    m = re.match(r"_ZN\d+\w+?(\d+)(k_\w+)", name)
+    if m:
+        return m.group(2)[:int(m.group(1))]
+    base = name.split("(")[0].split("<")[0]
+    return base.split("::")[-1].split()[-1]
+
+
 def kernel_key(name):
     if "k_score_mf" in name or "k_mf_cands" in name:   # mangled names in the rocprof CSV
         return "ransac_score"
@@ -40,19 +50,30 @@ WORKLOADS = {"c2": (8, 8, 128, "fp32"), "c3": (4, 8, 128, "bf16"), "c4": (8, 4, 
 
 
 def main(src, dst, config="c2"):
+    # per (path key, kernel): one list of per-dispatch values per counter.  A
+    # path key can hold several kernels of one step (ransac_score = k_mf_cands
+    # + k_score_mf2, one launch each): its per-step figure is the SUM of the
+    # kernels' per-dispatch means (round 2's summaries averaged the
+    # dispatches of both kernels together, which halved the scoring traffic)
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True)):
         acc = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
             k = kernel_key(r["Kernel_Name"])
             if k:
-                acc[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-        for (k, _, c), v in acc.items():
-            per[k][c].append(v)
+                acc[(k, r["Kernel_Name"], r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        for (k, name, _, c), v in acc.items():
+            per[(k, name)][c].append(v)
+    keys = collections.defaultdict(list)
+    for (k, name) in per:
+        keys[k].append(name)
     out = {}
-    for k, cs in per.items():
-        m = {c: sum(v) / len(v) for c, v in cs.items()}   # mean over dispatches
-        d = {"launches_sampled": max(len(v) for v in cs.values())}
+    for k, names in keys.items():
+        m = collections.defaultdict(float)
+        for name in names:
+            for c, v in per[(k, name)].items():
+                m[c] += sum(v) / len(v)                       # mean over this kernel's dispatches
+        d = {"launches_sampled": {short_name(n): max(len(v) for v in per[(k, n)].values()) for n in names}}
         d.update({c: round(v, 1) for c, v in sorted(m.items())})
         if "FETCH_SIZE" in m:
             d["hbm_read_bytes"] = int(m["FETCH_SIZE"] * 1024 * 2)
