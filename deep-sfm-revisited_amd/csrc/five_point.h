@@ -874,159 +874,113 @@ __device__ __forceinline__ void isolate_r(const SturmR& S, double lo, double hi,
 // ---------------------------------------------------------------------------
 // Split isolation (k_roots_split, tuning key roots_split = 1, default).
 //
-// isolate_r above advances each lane through pops, bisections and
-// regula-falsi steps in one loop, so every pass pays for all three whenever
-// any lane of the wave is in each mode, and a wave lasts as long as its
-// busiest hypothesis (p50 11 Sturm evaluations + 38 falsi steps, p99 89 + 70:
-// scripts/roots_stats.py).  The falsi refinement of an isolated single-root
-// interval depends on nothing but the interval and the polynomial, and its
-// root lands at a fixed slot (ioff), so the work is split in phases:
-//   1. each hypothesis lane runs the isolation with the bisections and
-//      modrf's case analysis and end-point evaluations, but where isolate_r
-//      would enter the falsi loop it appends a task (a, b, f(a), f(b), the
-//      interval, its slot) to the wave's task list in LDS;
-//   2. all 64 lanes of the wave then run the falsi loop over the task list,
-//      each lane claiming the next task when its own ends (a ballot and a
-//      prefix count, no atomics): one kind of step per pass, and the ~77
-//      tasks of a 32-hypothesis wave spread over 64 lanes;
-//   3. a task whose falsi loop gives up (modrf_pos's iteration limit: the
-//      reference then bisects the interval with the Sturm sequence) goes
-//      back to its hypothesis lane, which holds the sequence in registers.
-// Every interval sees exactly the reference's operations in their order, and
+// isolate_r above advances each lane through pops (with modrf's case analysis
+// and end-point evaluations), bisections and regula-falsi steps in one loop,
+// so every pass pays for all of them whenever any lane of the wave is in each
+// mode, and a wave lasts as long as its busiest hypothesis (p50 11 Sturm
+// evaluations + 38 falsi steps, p99 89 + 70: scripts/roots_stats.py).  What
+// happens to an isolated single-root interval depends on nothing but the
+// interval, its sign-change count and the sequence, and its root lands at a
+// fixed slot (ioff), so the work is split in phases:
+//   1. each hypothesis lane runs the isolation (the multi-root bisections),
+//      and where isolate_r would call modrf on a single-root node it appends
+//      the node (interval, count, slot) to the wave's task list in LDS;
+//   2. all 64 lanes of the wave then run modrf over the task list -- the case
+//      analysis and end-point evaluations when a lane claims a task, then one
+//      regula-falsi step per pass -- each lane claiming the next task when its
+//      own ends (a ballot and a prefix count, no atomics): the ~77 tasks of a
+//      32-hypothesis wave spread over 64 lanes;
+//   3. a node where modrf fails (end points of equal sign: 20 % of the
+//      hypotheses have one, scripts/roots_split_stats.py) or gives up (its
+//      iteration limit) goes back to its hypothesis lane, which holds the
+//      Sturm sequence in registers, for sbisect's bisection.
+// Every node sees exactly the reference's operations in their order, and
 // roots are written to their slot, so the roots are bit-identical to
-// isolate_r's (tests/test_gpu_ransac.py, test_gpu_solve.py: solve5.npz).
+// isolate_r's (tests/test_gpu_roots_split.py: the whole workspace).
 // ---------------------------------------------------------------------------
 constexpr int kRootTasks = kStkLanes * 10;   // a hypothesis has at most 10 isolated roots
-constexpr int kTaskDefer = 1 << 20;          // tmeta flag: falsi gave up, bisect on the owner lane
 struct RootsShared {                         // one wave's LDS (k_roots_split: one wave per block)
-  double ta[kRootTasks], tb[kRootTasks], tfa[kRootTasks], tfb[kRootTasks];   // falsi start
-  double tmn[kRootTasks], tmx[kRootTasks];   // the node's interval (the bisection fallback)
-  int tmeta[kRootTasks];                     // owner lane | ioff << 8 | inv << 16 | kTaskDefer
-  int tatlo[kRootTasks];                     // sign changes at the node's low end
-  double poly[11][kStkLanes];                // each hypothesis' s[0]
+  double seq[kSturmRegs][kStkLanes];         // each hypothesis' Sturm sequence (s[0] = c[0..10])
+  int np[kStkLanes];
+  double tmn[kRootTasks], tmx[kRootTasks];   // single-root nodes: interval
+  int tatlo[kRootTasks];                     // sign changes at its low end
+  int tmeta[kRootTasks];                     // owner lane | ioff << 8
+  int dlist[kRootTasks];                     // nodes for sbisect's bisection (phase 3)
   double roots[10][kStkLanes];               // root slots (scaled), 0 where none is found
-  int ntask, ndefer;
+  int ntask, ndl;
 };
 
-// phase 1: isolate_r with the falsi loop replaced by a task append
+// isolate_p1's work stack: IsoStack with the four small integers packed in one
+// word (sign-change counts and slots <= 10, depth <= kMaxDepth + 1)
+struct IsoStackP {
+  double* lohi;   // [kStkDepth][2][kStkLanes] + lane
+  int* meta;      // [kStkDepth][kStkLanes] + lane
+  __device__ __forceinline__ void put(int i, double lo, double hi, int atlo, int athi, int off, int depth) const {
+    lohi[(2 * i) * kStkLanes] = lo;
+    lohi[(2 * i + 1) * kStkLanes] = hi;
+    meta[i * kStkLanes] = atlo | (athi << 8) | (off << 16) | (depth << 24);
+  }
+};
+
+// phase 1: isolate_r's multi-root bisections; single-root nodes become tasks
 __device__ __forceinline__ void isolate_p1(const SturmR& S, double lo, double hi, int atlo, int athi,
-                                           const IsoStack& stk, RootsShared& sh, int lane) {
-  constexpr int kPop = 0, kBis1 = 2, kBisN = 3;
-  const double* c = S.c;
+                                           const IsoStackP& stk, RootsShared& sh, int lane) {
   int sp = 0;
   stk.put(sp++, lo, hi, atlo, athi, 0, 0);
-  int mode = kPop, it = 0;
-  int iatlo = 0, iathi = 0, ioff = 0, idepth = 0;
-  double mn = 0.0, mx = 0.0, mid = 0.0;
+  bool bis = false;
+  int it = 0, iatlo = 0, iathi = 0, ioff = 0, idepth = 0;
+  double mn = 0.0, mx = 0.0;
   for (;;) {
-    if (mode == kPop) {
+    if (!bis) {
       if (sp == 0) break;
       --sp;
       mn = stk.lohi[(2 * sp) * kStkLanes];
       mx = stk.lohi[(2 * sp + 1) * kStkLanes];
-      iatlo = stk.ints[(4 * sp) * kStkLanes];
-      iathi = stk.ints[(4 * sp + 1) * kStkLanes];
-      ioff = stk.ints[(4 * sp + 2) * kStkLanes];
-      idepth = stk.ints[(4 * sp + 3) * kStkLanes];
+      const int m = stk.meta[sp * kStkLanes];
+      iatlo = m & 0xff;
+      iathi = (m >> 8) & 0xff;
+      ioff = (m >> 16) & 0xff;
+      idepth = m >> 24;
       if (idepth >= kMaxDepth) continue;
       it = 0;
       if (iatlo - iathi != 1) {
-        mode = kBisN;
+        bis = true;
       } else {
-        double a = mn, b = mx, fa, fb;
-        bool inv;
-        if (a > b) { const double t = a; a = b; b = t; }
-        if (b <= 1.0 && a >= -1.0) {
-          inv = false;
-        } else if (a >= 1.0 || b <= -1.0) {
-          inv = true;
-        } else {
-          double fp1 = 0.0, fm1 = 0.0, ga = 0.0, gb = 0.0;
-#pragma unroll
-          for (int i = 9; i >= 0; --i) {
-            fp1 = c[i] + fp1;
-            fm1 = c[i] - fm1;
-            ga = a * ga + c[i];
-            gb = b * gb + c[i];
-          }
-          if (a < -1.0 && b > 1.0) {
-            if (ga * fm1 < 0.0) { b = -1.0; inv = true; }
-            else if (gb * fp1 < 0.0) { a = 1.0; inv = true; }
-            else { a = -1.0; b = 1.0; inv = false; }
-          } else if (a < -1.0) {
-            if (ga * fm1 < 0.0) { b = -1.0; inv = true; }
-            else { a = -1.0; inv = false; }
-          } else {
-            if (gb * fp1 < 0.0) { a = 1.0; inv = true; }
-            else { b = 1.0; inv = false; }
-          }
-        }
-        if (inv) { const double t = a; a = 1.0 / b; b = 1.0 / t; }
-        if (inv) {
-          fa = fb = c[0];
-#pragma unroll
-          for (int i = 1; i <= 10; ++i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
-        } else {
-          fa = fb = c[10];
-#pragma unroll
-          for (int i = 9; i >= 0; --i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
-        }
-        if (fa * fb > 0.0) {
-          mode = kBis1;                                        // modrf failed: bisection on [mn, mx]
-        } else if (fabs(fa) < kRelErr) {
-          sh.roots[ioff][lane] = inv ? 1.0 / a : a;           // stays kPop
-        } else if (fabs(fb) < kRelErr) {
-          sh.roots[ioff][lane] = inv ? 1.0 / b : b;
-        } else {
-          const int t = atomicAdd(&sh.ntask, 1);               // the falsi loop: phase 2
-          sh.ta[t] = a;
-          sh.tb[t] = b;
-          sh.tfa[t] = fa;
-          sh.tfb[t] = fb;
-          sh.tmn[t] = mn;
-          sh.tmx[t] = mx;
-          sh.tmeta[t] = lane | (ioff << 8) | (inv ? 1 << 16 : 0);
-          sh.tatlo[t] = iatlo;
-        }
+        const int t = atomicAdd(&sh.ntask, 1);                 // modrf: phase 2
+        sh.tmn[t] = mn;
+        sh.tmx[t] = mx;
+        sh.tatlo[t] = iatlo;
+        sh.tmeta[t] = lane | (ioff << 8);
       }
     }
-    if (mode >= kBis1) {
-      mid = (double)((mn + mx) / 2);
-      bool stop = false;
-      if (mode == kBis1) {
-        if (fabs(mid) > kRelErr) stop = fabs((mx - mn) / mid) < kRelErr;
-        else stop = fabs(mx - mn) < kRelErr;
-      }
-      if (!stop) {
-        const int atmid = sign_changes_r(S, mid);
-        if (mode == kBis1) {
-          if ((iatlo - atmid) == 0) mn = mid; else mx = mid;
-          stop = ++it == kMaxIt;
-        } else {
-          const int n1 = iatlo - atmid, n2 = atmid - iathi;
-          if (n1 != 0 && n2 != 0) {
-            if (sp + 2 <= kStkDepth) {
-              stk.put(sp++, mid, mx, atmid, iathi, ioff + n1, idepth + 1);
-              stk.put(sp++, mn, mid, iatlo, atmid, ioff, idepth + 1);
-            }
-            mode = kPop;
-          } else {
-            const bool fixed = (n1 == 0) ? mid == mn : mid == mx;
-            if (n1 == 0) mn = mid; else mx = mid;
-            if (fixed) it = kMaxIt - 1;
-            if (++it == kMaxIt) {
-              for (int r = iathi; r < iatlo; ++r) sh.roots[ioff + r - iathi][lane] = mid;
-              mode = kPop;
-            }
-          }
+    if (bis) {
+      const double mid = (double)((mn + mx) / 2);
+      const int atmid = sign_changes_r(S, mid);
+      const int n1 = iatlo - atmid, n2 = atmid - iathi;
+      if (n1 != 0 && n2 != 0) {
+        if (sp + 2 <= kStkDepth) {
+          stk.put(sp++, mid, mx, atmid, iathi, ioff + n1, idepth + 1);
+          stk.put(sp++, mn, mid, iatlo, atmid, ioff, idepth + 1);
+        }
+        bis = false;
+      } else {
+        // An interval that no longer changes (it has shrunk to adjacent
+        // doubles around a multiple root) repeats this step until the
+        // iteration limit, with the same mid: jump to the limit.
+        const bool fixed = (n1 == 0) ? mid == mn : mid == mx;
+        if (n1 == 0) mn = mid; else mx = mid;
+        if (fixed) it = kMaxIt - 1;
+        if (++it == kMaxIt) {
+          for (int r = iathi; r < iatlo; ++r) sh.roots[ioff + r - iathi][lane] = mid;
+          bis = false;
         }
       }
-      if (stop) { sh.roots[ioff][lane] = mid; mode = kPop; }
     }
   }
 }
 
-// phase 2: modrf_pos's loop (sturm.cu:82-205) over the wave's task list, on every lane
+// phase 2: modrf (sturm.cu:208-275) and modrf_pos's loop (43-205) over the
+// wave's task list, on every lane
 __device__ __forceinline__ void falsi_tasks(RootsShared& sh, int lane) {
   const int ntask = sh.ntask;
   int next = 0, cur = -1, it = 0, owner = 0, ioff = 0;
@@ -1038,25 +992,72 @@ __device__ __forceinline__ void falsi_tasks(RootsShared& sh, int lane) {
   for (;;) {
     const unsigned long long idle = __ballot(cur < 0);
     const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(idle >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)idle, 0u));
+    bool fresh = false;
     if (cur < 0 && next + rank < ntask) {
       cur = next + rank;
-      a = sh.ta[cur];
-      b = sh.tb[cur];
-      fa = sh.tfa[cur];
-      fb = sh.tfb[cur];
-      lfx = fa;
-      const int m = sh.tmeta[cur];
-      owner = m & 0xff;
-      ioff = (m >> 8) & 0xff;
-      inv = (m >> 16) & 1;
-      it = 0;
-#pragma unroll
-      for (int i = 0; i <= 10; ++i) c[i] = sh.poly[i][owner];
+      fresh = true;
     }
     next += __popcll(idle);
     if (__ballot(cur >= 0) == 0ull) break;
+    if (fresh) {
+      const int m = sh.tmeta[cur];
+      owner = m & 0xff;
+      ioff = m >> 8;
+#pragma unroll
+      for (int i = 0; i <= 10; ++i) c[i] = sh.seq[i][owner];
+      // modrf: pick (a, b, inverted), then modrf_pos's end-point evaluations
+      a = sh.tmn[cur];
+      b = sh.tmx[cur];
+      if (a > b) { const double t = a; a = b; b = t; }
+      if (b <= 1.0 && a >= -1.0) {
+        inv = false;
+      } else if (a >= 1.0 || b <= -1.0) {
+        inv = true;
+      } else {
+        double fp1 = 0.0, fm1 = 0.0, ga = 0.0, gb = 0.0;
+#pragma unroll
+        for (int i = 9; i >= 0; --i) {
+          fp1 = c[i] + fp1;
+          fm1 = c[i] - fm1;
+          ga = a * ga + c[i];
+          gb = b * gb + c[i];
+        }
+        if (a < -1.0 && b > 1.0) {
+          if (ga * fm1 < 0.0) { b = -1.0; inv = true; }
+          else if (gb * fp1 < 0.0) { a = 1.0; inv = true; }
+          else { a = -1.0; b = 1.0; inv = false; }
+        } else if (a < -1.0) {
+          if (ga * fm1 < 0.0) { b = -1.0; inv = true; }
+          else { a = -1.0; inv = false; }
+        } else {
+          if (gb * fp1 < 0.0) { a = 1.0; inv = true; }
+          else { b = 1.0; inv = false; }
+        }
+      }
+      if (inv) { const double t = a; a = 1.0 / b; b = 1.0 / t; }
+      if (inv) {
+        fa = fb = c[0];
+#pragma unroll
+        for (int i = 1; i <= 10; ++i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
+      } else {
+        fa = fb = c[10];
+#pragma unroll
+        for (int i = 9; i >= 0; --i) { fa = a * fa + c[i]; fb = b * fb + c[i]; }
+      }
+      lfx = fa;
+      it = 0;
+      if (fa * fb > 0.0) {                                      // modrf failed: phase 3
+        sh.dlist[atomicAdd(&sh.ndl, 1)] = cur;
+        cur = -1;
+      } else if (fabs(fa) < kRelErr) {
+        sh.roots[ioff][owner] = inv ? 1.0 / a : a;
+        cur = -1;
+      } else if (fabs(fb) < kRelErr) {
+        sh.roots[ioff][owner] = inv ? 1.0 / b : b;
+        cur = -1;
+      }
+    }
     if (cur >= 0) {
-      ROOTS_COUNT(g_roots_falsi);
       const double x = (fb * a - fa * b) / (fb - fa);
       double fx;
       if (inv) {
@@ -1080,9 +1081,8 @@ __device__ __forceinline__ void falsi_tasks(RootsShared& sh, int lane) {
           v = a;
         } else {
           lfx = fx;
-          if (++it == kMaxIt) {                                // modrf_pos gave up: phase 3
-            sh.tmeta[cur] |= kTaskDefer;
-            sh.ndefer = 1;
+          if (++it == kMaxIt) {                                 // modrf_pos gave up: phase 3
+            sh.dlist[atomicAdd(&sh.ndl, 1)] = cur;
             cur = -1;
           }
         }
@@ -1095,28 +1095,86 @@ __device__ __forceinline__ void falsi_tasks(RootsShared& sh, int lane) {
   }
 }
 
-// phase 3: sbisect's bisection after a failed modrf, on the owner lane (sturm.cu:465-497)
-__device__ __forceinline__ void bisect_deferred(const SturmR& S, RootsShared& sh, int lane) {
-  const int ntask = sh.ntask;
-  for (int t = 0; t < ntask; ++t) {
-    const int m = sh.tmeta[t];
-    if (!(m & kTaskDefer) || (m & 0xff) != lane) continue;
-    double mn = sh.tmn[t], mx = sh.tmx[t], mid;
-    const int iatlo = sh.tatlo[t];
-    int it = 0;
-    for (;;) {
-      mid = (double)((mn + mx) / 2);
-      bool stop;
-      if (fabs(mid) > kRelErr) stop = fabs((mx - mn) / mid) < kRelErr;
-      else stop = fabs(mx - mn) < kRelErr;
-      if (!stop) {
-        const int atmid = sign_changes_r(S, mid);
-        if ((iatlo - atmid) == 0) mn = mid; else mx = mid;
-        stop = ++it == kMaxIt;
-      }
-      if (stop) break;
+// phase 3: sbisect's bisection after modrf (sturm.cu:465-497), speculated
+// three levels deep.  Lanes form groups of 8; a group takes one node of the
+// list and, each pass, its lanes 0..6 evaluate the Sturm sequence at the
+// 7 midpoints of the next three bisection levels (heap order: lane 0 the
+// current midpoint, lanes 1 / 2 its left / right halves' midpoints, ...).  A
+// midpoint is computed from its interval exactly as the sequential loop
+// would reach it, so the walk down the tree (the stop tests, the sign-change
+// decision, the iteration limit) reproduces the sequential bisection's
+// steps and its final midpoint bit for bit, three steps per pass.
+__device__ __forceinline__ void bisect_deferred(RootsShared& sh, int lane) {
+  const int ndl = sh.ndl;
+  if (ndl == 0) return;
+  const int j = lane & 7, gbase = lane & ~7;
+  int next = 0, cur = -1, it = 0, iatlo = 0, owner = 0, ioff = 0;
+  double mn = 0.0, mx = 0.0;
+  SturmR T;
+  for (;;) {
+    // the leader (j == 0) of each idle group claims the next node, in group order
+    const unsigned long long idle = __ballot(cur < 0 && j == 0);
+    const unsigned long long below = gbase == 0 ? 0ull : (idle & ((1ull << gbase) - 1ull));
+    const int t = next + __popcll(below);
+    if (cur < 0 && t < ndl) {
+      cur = sh.dlist[t];
+      mn = sh.tmn[cur];
+      mx = sh.tmx[cur];
+      iatlo = sh.tatlo[cur];
+      owner = sh.tmeta[cur] & 0xff;
+      ioff = sh.tmeta[cur] >> 8;
+      it = 0;
+#pragma unroll
+      for (int i = 0; i < kSturmRegs; ++i) T.c[i] = sh.seq[i][owner];
+      T.np = sh.np[owner];
     }
-    sh.roots[(m >> 8) & 0xff][lane] = mid;
+    next += __popcll(idle);
+    if (__ballot(cur >= 0) == 0ull) break;
+    // this lane's node: its interval down the heap path from [mn, mx]
+    double lo = mn, hi = mx;
+    const int k = j < 7 ? j : 0;
+    const int depth = k == 0 ? 0 : (k < 3 ? 1 : 2);
+    for (int d = depth - 1; d >= 0; --d) {
+      // bit d of (k + 1) below its leading one: 0 = left half, 1 = right half
+      const double m = (double)((lo + hi) / 2);
+      if (((k + 1) >> d) & 1) lo = m; else hi = m;
+    }
+    const double mid = (double)((lo + hi) / 2);
+    bool stop;
+    if (fabs(mid) > kRelErr) stop = fabs((hi - lo) / mid) < kRelErr;
+    else stop = fabs(hi - lo) < kRelErr;
+    int atmid = 0;
+    if (cur >= 0 && j < 7 && !stop) {
+      ROOTS_COUNT(g_roots_falsi);                            // split stats: Sturm evaluations of phase 3
+      atmid = sign_changes_r(T, mid);
+    }
+    // the walk, the same in every lane of the group
+    int node = 0;
+    bool done = false;
+    double root = 0.0;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int src = gbase + node;
+      const double m = __shfl(mid, src);
+      const bool st = __shfl((int)stop, src) != 0;
+      const int am = __shfl(atmid, src);
+      if (cur >= 0 && !done) {
+        if (st) {
+          done = true;
+          root = m;
+        } else {
+          if ((iatlo - am) == 0) { mn = m; node = 2 * node + 2; } else { mx = m; node = 2 * node + 1; }
+          if (++it == kMaxIt) {
+            done = true;
+            root = m;
+          }
+        }
+      }
+    }
+    if (cur >= 0 && done) {
+      if (j == 0) sh.roots[ioff][owner] = root;
+      cur = -1;
+    }
   }
 }
 
@@ -1193,7 +1251,7 @@ __device__ __forceinline__ int count_real_roots_r(const SturmR& R, int* atneg, i
 // sequence for phase 3.
 template <bool SPLIT>
 __device__ __forceinline__ int real_roots_t(const double poly[11], double roots[10], const IsoStack& stk, SturmR& R,
-                                            RootsShared* sh, int lane, double* fac_out) {
+                                            RootsShared* sh, const IsoStackP* stk_p, int lane, double* fac_out) {
 #ifdef SFM_ROOTS_STATS
   unsigned long long ts = __builtin_amdgcn_s_memtime();
 #endif
@@ -1246,8 +1304,9 @@ __device__ __forceinline__ int real_roots_t(const double poly[11], double roots[
     if constexpr (SPLIT) {
       *fac_out = fac;
 #pragma unroll
-      for (int i = 0; i <= 10; ++i) sh->poly[i][lane] = R.c[i];
-      isolate_p1(R, mn, mx, atmin, atmax, stk, *sh, lane);
+      for (int i = 0; i < kSturmRegs; ++i) sh->seq[i][lane] = R.c[i];
+      sh->np[lane] = R.np;
+      isolate_p1(R, mn, mx, atmin, atmax, *stk_p, *sh, lane);
     } else {
       isolate_r(R, mn, mx, atmin, atmax, roots, stk);
       for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
@@ -1292,8 +1351,9 @@ __device__ __forceinline__ int real_roots_t(const double poly[11], double roots[
     if constexpr (SPLIT) {
       *fac_out = fac;
 #pragma unroll
-      for (int i = 0; i <= 10; ++i) sh->poly[i][lane] = R.c[i];
-      isolate_p1(R, mn, mx, atmin, atmax, stk, *sh, lane);
+      for (int i = 0; i < kSturmRegs; ++i) sh->seq[i][lane] = R.c[i];
+      sh->np[lane] = R.np;
+      isolate_p1(R, mn, mx, atmin, atmax, *stk_p, *sh, lane);
     } else {
       isolate_r(R, mn, mx, atmin, atmax, roots, stk);
       for (int i = 0; i < nr && i < 10; ++i) roots[i] /= fac;
@@ -1304,7 +1364,7 @@ __device__ __forceinline__ int real_roots_t(const double poly[11], double roots[
 
 __device__ __forceinline__ int real_roots_r(const double poly[11], double roots[10], const IsoStack& stk) {
   SturmR R;
-  return real_roots_t<false>(poly, roots, stk, R, nullptr, 0, nullptr);
+  return real_roots_t<false>(poly, roots, stk, R, nullptr, nullptr, 0, nullptr);
 }
 
 // null_space_solve_3x3_half_pivot (essential_matrix_5pt.cu:476-507)

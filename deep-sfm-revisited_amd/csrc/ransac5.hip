@@ -1668,19 +1668,18 @@ __global__ __launch_bounds__(64) void k_roots_split(int H, int lanes, double* __
   const int h = blockIdx.x * lanes + lane;
   const bool own = lane < lanes && h < H;
   __shared__ double s_lohi[kStkDepth * 2 * kStkLanes];
-  __shared__ int s_ints[kStkDepth * 4 * kStkLanes];
+  __shared__ int s_meta[kStkDepth * kStkLanes];
   __shared__ RootsShared sh;
   if (lane < kStkLanes) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) sh.roots[i][lane] = 0.0;
   }
-  if (lane == 0) { sh.ntask = 0; sh.ndefer = 0; }
+  if (lane == 0) { sh.ntask = 0; sh.ndl = 0; }
   __syncthreads();
 #ifdef SFM_ROOTS_STATS
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
   const size_t hb = (size_t)b * H + h;
-  SturmR R;
   int nr = 0;
   double fac = 1.0;
   if (own) {
@@ -1688,16 +1687,24 @@ __global__ __launch_bounds__(64) void k_roots_split(int H, int lanes, double* __
 #pragma unroll
     for (int i = 0; i <= 10; ++i) poly[i] = st_at(st, stride, kStPoly + i, hb);
     double roots[10];
-    const IsoStack stk{s_lohi + lane, s_ints + lane};
-    nr = real_roots_t<true>(poly, roots, stk, R, &sh, lane, &fac);
+    SturmR R;
+    const IsoStack stk{nullptr, nullptr};
+    const IsoStackP stkp{s_lohi + lane, s_meta + lane};
+    nr = real_roots_t<true>(poly, roots, stk, R, &sh, &stkp, lane, &fac);
   }
+#ifdef SFM_ROOTS_STATS
+  // split stats: cycles at the end of phase 1 / phase 2 in the second half of g_roots_cycles / g_roots_phase[0]
+  const size_t si = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+  if (own) g_roots_cycles[si + (1 << 16)] = __builtin_amdgcn_s_memtime() - t0;
+#endif
   __syncthreads();
   falsi_tasks(sh, lane);
   __syncthreads();
-  if (sh.ndefer) {
-    if (own) bisect_deferred(R, sh, lane);
-    __syncthreads();
-  }
+#ifdef SFM_ROOTS_STATS
+  if (own) g_roots_phase[0][si] = __builtin_amdgcn_s_memtime() - t0;
+#endif
+  bisect_deferred(sh, lane);
+  __syncthreads();
   if (own) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
@@ -1708,9 +1715,7 @@ __global__ __launch_bounds__(64) void k_roots_split(int H, int lanes, double* __
     out_nroots[hb] = nr;
   }
 #ifdef SFM_ROOTS_STATS
-  if (own)
-    g_roots_cycles[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x] =
-        __builtin_amdgcn_s_memtime() - t0;
+  if (own) g_roots_cycles[si] = __builtin_amdgcn_s_memtime() - t0;
 #endif
 }
 
