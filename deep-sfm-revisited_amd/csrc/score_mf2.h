@@ -42,12 +42,16 @@
 #ifndef SFM_MF2_WAVES
 #define SFM_MF2_WAVES 12
 #endif
+#ifndef SFM_MF2_CARRY
+#define SFM_MF2_CARRY 0
+#endif
 constexpr int kMf2Waves = SFM_MF2_WAVES;       // 12: 3 per SIMD, two accumulator sets; 16: 4 per SIMD, one
 constexpr int kMf2Wpe = kMf2Waves / 4;
 constexpr int kMf2Span = SFM_MF2_SPAN;         // points per staged span
 constexpr int kMf2Tiles = kMf2Span / 32;       // tiles per span (every run decides all of them)
 constexpr int kMf2Queue = kMf2Waves > 12 ? 256 : 512;   // undecided entries per wave and drain window (LDS)
 static_assert(kMf2Tiles <= 32 && kMf2Tiles % 2 == 0, "32-bit decision strings, tiles in pairs");
+static_assert(!SFM_MF2_CARRY || kMf2Span == 1024, "carried queue entries hold a 10-bit point");
 
 #ifdef SFM_MF_STATS
 // experiment builds only: [0] undecided evaluations, [1] evaluations decided by the tile loop
@@ -71,6 +75,30 @@ __device__ __forceinline__ void mf2_drain(const double* __restrict__ Erow0, cons
     const uint32_t e = q[i];
     const int c = (int)(e >> 24), r = (int)(e & 0xffffffu);
     if (inlier_f64v(Erow0 + (size_t)c * kCandStride, spts[r], kc)) atomicAdd(&cnt[c], 1);
+  }
+}
+
+// SFM_MF2_CARRY: the queue outlives the run.  Entries carry their candidate
+// tile (k << 15 | row << 10 | span-relative point), each run drains only
+// whole 64-entry rounds and keeps the rest for the next run of the same span
+// (the span's points stay staged), and inliers go straight to the pair's
+// global counts.  A run has ~67 undecided evaluations at the bench threshold
+// (0.2 %), so the per-run drain took two rounds, the second nearly empty.
+// Measured slower and off by default (profiles/r03_mf2_carry_ab.txt: 5.93-5.97
+// vs 5.71-5.75 ms): the drain's global atomics sit in the wave's vmcnt queue
+// ahead of the next run's A-row loads, so the prefetch wait grew by more
+// (stamps 2.2 -> 6.4 %) than the drain shrank (11.7 -> 4.7 %).
+__device__ __forceinline__ void mf2_drain_g(const double* __restrict__ Eb, const double4* __restrict__ spts,
+                                            const ScoreConsts& kc, int lane, int32_t* __restrict__ cT,
+                                            int32_t* __restrict__ cR, const uint32_t* q, int qn) {
+#pragma unroll 1
+  for (int i = lane; i < qn; i += 64) {
+    const uint32_t e = q[i];
+    const int c = (int)(e >> 15) * kKC + (int)((e >> 10) & 31u), r = (int)(e & 1023u);
+    if (inlier_f64v(Eb + (size_t)c * kCandStride, spts[r], kc)) {
+      atomicAdd(cT + c, 1);
+      atomicAdd(cR + c, 1);
+    }
   }
 }
 
@@ -134,7 +162,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   const int logical = (G % 8 == 0) ? (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const long long U = s_first[batch];
   const long long u_beg = U * logical / G, u_end = U * (logical + 1) / G;
+#if !SFM_MF2_CARRY
   int32_t* cnt = s_cnt[wv];
+#endif
   uint32_t* queue = s_queue[wv];
   const _Float16* fr = &s_frag[0][0][0][0];
   constexpr int kTileHalves = 3 * 64 * 8;
@@ -205,6 +235,12 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     int k = claim();
     const int ctot = __builtin_amdgcn_readfirstlane(s_ctot[b]);   // the pair's candidates, in an SGPR
     if (k < k1) load_rows(b, k, ctot);
+#if SFM_MF2_CARRY
+    int qn = 0;                                               // carried queue entries (wave-uniform)
+    const double* Eb = candE + (size_t)b * cmax * kCandStride;
+    int32_t* cTb = cntT + (size_t)b * cmax;
+    int32_t* cRb = cntR + (size_t)b * cmax;
+#endif
 #pragma unroll 1
     while (k < k1) {
 #ifdef SFM_MF_STAMPS
@@ -274,6 +310,59 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         atomicAdd(&g_mf2_stats[1], (unsigned long long)kKC * kMf2Span);
       }
 #endif
+#if SFM_MF2_CARRY
+      if (qn + qtotal <= kMf2Queue) {
+        uint32_t* q = queue + qn + (incl - nl);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          uint32_t uu = ~(s1[g] | s2[g]);
+          const uint32_t top = ((uint32_t)k << 15) | ((uint32_t)mf_row(g, hl) << 10) |
+                               (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+          while (uu) {
+            *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
+            uu &= uu - 1u;
+          }
+        }
+        qn += qtotal;
+        wave_sync();
+        MF_STAMP(2);
+        if (qn >= 64) {
+          const int nd = qn & ~63;
+          mf2_drain_g(Eb, s_pts, kc, lane, cTb, cRb, queue, nd);
+          uint32_t keep = 0u;
+          if (lane < qn - nd) keep = queue[nd + lane];
+          wave_sync();
+          if (lane < qn - nd) queue[lane] = keep;
+          wave_sync();
+          qn -= nd;
+        }
+        MF_STAMP(3);
+      } else {
+        // more than the queue holds: drain the carry, then this run in windows
+        mf2_drain_g(Eb, s_pts, kc, lane, cTb, cRb, queue, qn);
+        qn = 0;
+        wave_sync();
+        for (int base = 0; base < qtotal; base += kMf2Queue) {
+          int pos = incl - nl - base;
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            uint32_t uu = ~(s1[g] | s2[g]);
+            const uint32_t top = ((uint32_t)k << 15) | ((uint32_t)mf_row(g, hl) << 10) |
+                                 (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+            while (uu) {
+              if (pos >= 0 && pos < kMf2Queue) queue[pos] = top - 32u * (uint32_t)__builtin_ctz(uu);
+              uu &= uu - 1u;
+              ++pos;
+            }
+          }
+          wave_sync();
+          MF_STAMP(2);
+          mf2_drain_g(Eb, s_pts, kc, lane, cTb, cRb, queue, min(kMf2Queue, qtotal - base));
+          wave_sync();
+          MF_STAMP(3);
+        }
+      }
+#else
       const double* Erow0 = candE + ((size_t)b * cmax + c0) * kCandStride;
       for (int base = 0; base < qtotal; base += kMf2Queue) {
         int pos = incl - nl - base;
@@ -307,6 +396,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         MF_STAMP(3);
       }
       MF_STAMP(2);
+#endif
       // 4. counts: popcounts of the inlier strings over the 32 points of each half + the float64 counts
       int cT[16];
 #pragma unroll
@@ -314,8 +404,12 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       const int sumT = mf_half_reduce(cT, lane);
       if ((lane & 1) == 0) {
         const int c = mf_row((rl >> 1) & 15, hl);
+#if SFM_MF2_CARRY
+        const int d = sumT;
+#else
         const int d = sumT + cnt[c];
         cnt[c] = 0;
+#endif
         if (d && c0 + c < ctot) {
           atomicAdd(cntT + (size_t)b * cmax + c0 + c, d);
           atomicAdd(cntR + (size_t)b * cmax + c0 + c, d);
@@ -325,12 +419,18 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       MF_STAMP(4);
       k = kn;
     }
+#if SFM_MF2_CARRY
+    if (qn) {                                                 // the span's last entries, before it is re-staged
+      mf2_drain_g(Eb, s_pts, kc, mf2_lane(), cTb, cRb, queue, qn);
+      wave_sync();
+    }
+#endif
     u += k1 - k0;
     lds_barrier();                                            // the span is re-staged next
     MF_STAMP(5);
   }
 #ifdef SFM_MF_STAMPS
-  if (lane == 0)
+  if (mf2_lane() == 0)
     for (int i = 0; i < kMfStamps; ++i) atomicAdd(&g_mf_stamps[i], mf_acc_[i]);
 #endif
 }
