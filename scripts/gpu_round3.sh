@@ -25,6 +25,13 @@ find gpurun_out/r3_prof_c2 -name "*kernel_stats*"
 if [ "${SKIP_PMC:-0}" != "1" ]; then
   CONFIG=c2 timeout -k 10 900 bash scripts/gpu_pmc.sh > gpurun_out/r3_pmc.log 2>&1 || { tail -20 gpurun_out/r3_pmc.log; exit 1; }
 fi
+if [ "${SKIP_PMC:-0}" != "1" ]; then
+  CONFIG=c3 PMC_OUT=gpurun_out/pmc_c3 timeout -k 10 900 bash scripts/gpu_pmc.sh > gpurun_out/r3_pmc_c3.log 2>&1 \
+      || { tail -20 gpurun_out/r3_pmc_c3.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r3_prof_c3 -o run --output-format csv -- \
+      python3 bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-regularize \
+      > gpurun_out/r3_prof_c3.log 2>&1 || { tail -20 gpurun_out/r3_prof_c3.log; exit 1; }
+fi
 for cfg in sparse c3 c4; do
   timeout -k 10 300 python -u bench.py --config $cfg --steps 20 --warmup 3 --no-cpu-baseline --no-regularize \
       > gpurun_out/r3_bench_$cfg.log 2>&1 || { tail -20 gpurun_out/r3_bench_$cfg.log; exit 1; }
