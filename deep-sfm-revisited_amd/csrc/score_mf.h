@@ -67,6 +67,25 @@
 #endif
 static_assert(SFM_MF_ACC_U <= 64, "the relative part K_acc |a'| must stay below the 2^-18 folded into t");
 
+// The AM-GM slack delta = 2^-SFM_MF_AMGM of the certain-inlier / outlier
+// tests above (2^-6 written out there, the round-2 value).  In general
+//   (|a| + alpha)^2 <= (1 + delta) a^2 + (1 + 1/delta) alpha^2,
+//   (|a| - alpha)^2 >= (1 - delta) a^2 - (1/delta - 1) alpha^2   (|a| >= alpha),
+// so t_lo = t / (1 + delta), eps1 = (1 + 1/delta) alpha^2 / (1 + delta),
+// t_hi = t / (1 - delta), eps2 = (1/delta) alpha^2 / (1 - delta) (>= the
+// (1/delta - 1) needed; with |a| < alpha the outlier test cannot fire since
+// eps2 > alpha^2 for delta <= 1/2).  delta trades the relative band (t_lo,
+// t_hi) against the alpha^2 terms; at the bench threshold 1e-4 the alpha^2
+// terms dominate and delta = 2^-5 minimises the undecided band
+// (scripts/band_width_model.py: 0.193 % at 2^-6, 0.145 % at 2^-5, 0.146 % at 2^-4).
+#ifndef SFM_MF_AMGM
+#define SFM_MF_AMGM 5
+#endif
+static_assert(SFM_MF_AMGM >= 1 && SFM_MF_AMGM <= 10, "delta in [2^-10, 1/2]");
+constexpr double kMfDelta = 1.0 / (double)(1 << SFM_MF_AMGM);
+constexpr double kMfPin = 1.0 + (double)(1 << SFM_MF_AMGM);    // 1 + 1/delta
+constexpr double kMfPout = (double)(1 << SFM_MF_AMGM);         // 1/delta
+
 typedef _Float16 mf_half8 __attribute__((ext_vector_type(8)));
 typedef float mf_float16 __attribute__((ext_vector_type(16)));
 
@@ -106,8 +125,8 @@ __host__ inline bool mf_params(double thr, MfParams* p) {
   while (k < 15 && std::ldexp(thr, k + 1) <= 1.0) ++k;          // 2^k <= 1/thr < 2^(k+1)
   const double t = std::ldexp(thr * thr, 2 * k);                 // in (0.25, 1]
   p->k = k;
-  p->t_lo = t * (1.0 - 0x1p-40) * (1.0 - 0x1p-22) * (1.0 - 0x1p-18) / (1.0 + 0x1p-6);
-  p->t_hi = t * (1.0 + 0x1p-40) * (1.0 + 0x1p-22) * (1.0 + 0x1p-18) / (1.0 - 0x1p-6);
+  p->t_lo = t * (1.0 - 0x1p-40) * (1.0 - 0x1p-22) * (1.0 - 0x1p-18) / (1.0 + kMfDelta);
+  p->t_hi = t * (1.0 + 0x1p-40) * (1.0 + 0x1p-22) * (1.0 + 0x1p-18) / (1.0 - kMfDelta);
   return true;
 }
 
@@ -205,12 +224,12 @@ __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, con
     const double K1 = aS * C1 + 0x1p-24, K2 = aS * C2 + 0x1p-24;
     const double K3 = aS * fabs(cc[8]) + 0x1p-24 + 9.0 * 0x1p-24 * cm;
     const double infl = 3.0 * (1.0 + 0x1p-9);
-    const double e1s1 = 16.0 * infl * 65.0 * K1 * K1 / (1.0 + 0x1p-6);     // x (s1/4)^2
-    const double e1s2 = 16.0 * infl * 65.0 * K2 * K2 / (1.0 + 0x1p-6);
-    const double e1c = infl * 65.0 * K3 * K3 / (1.0 + 0x1p-6);
-    const double e2s1 = 16.0 * infl * 64.0 * K1 * K1 / (1.0 - 0x1p-6);
-    const double e2s2 = 16.0 * infl * 64.0 * K2 * K2 / (1.0 - 0x1p-6);
-    const double e2c = infl * 64.0 * K3 * K3 / (1.0 - 0x1p-6);
+    const double e1s1 = 16.0 * infl * kMfPin * K1 * K1 / (1.0 + kMfDelta);     // x (s1/4)^2
+    const double e1s2 = 16.0 * infl * kMfPin * K2 * K2 / (1.0 + kMfDelta);
+    const double e1c = infl * kMfPin * K3 * K3 / (1.0 + kMfDelta);
+    const double e2s1 = 16.0 * infl * kMfPout * K1 * K1 / (1.0 - kMfDelta);
+    const double e2s2 = 16.0 * infl * kMfPout * K2 * K2 / (1.0 - kMfDelta);
+    const double e2c = infl * kMfPout * K3 * K3 / (1.0 - kMfDelta);
     // the constant monomial carries g_2 -/+ eps (its f16 rounding is covered by eta)
     row[32 + 2] = (_Float16)(float)(mp.t_lo * g[2] - e1c);
     row[48 + 2] = (_Float16)(float)(mp.t_hi * g[2] + e2c);
