@@ -82,6 +82,24 @@ static_assert(SFM_MF_ACC_U <= 64, "the relative part K_acc |a'| must stay below 
 #define SFM_MF_AMGM 5
 #endif
 static_assert(SFM_MF_AMGM >= 1 && SFM_MF_AMGM <= 10, "delta in [2^-10, 1/2]");
+
+// a^2 folded into the band MFMAs (k_score_mf2, score_mf2.h): there the
+// decisions are the signs of z1 = MFMA(C = aa, -Ylo rows) ~ aa - Ylo and
+// z2 = MFMA(C = aa, -Yhi rows) ~ aa - Yhi, aa = fl(a * a), instead of
+// fma(a, a, -Ylo) and fma(-a, a, Yhi).  The accumulator C = aa is one of the
+// n = 17 MFMA operands, so the accumulation adds <= K_acc aa (K_acc = 36u) to
+// the error already in eta, and aa itself rounds once (u):
+//   inlier  (z1 < 0; C = +0 and exact products never give -0):
+//     aa (1 - K_acc) < Ylo  =>  a^2 <= aa (1 + u) < Ylo (1 + 2^-18)   (Ylo > 0;
+//     else the test cannot fire), covered by t_lo * (1 - 2^-18) (the
+//     subtracted eps / eta terms only grow when scaled up);
+//   outlier (sign bit of z2 clear, z2 >= +0 -- ties included):
+//     aa (1 + K_acc) >= Yhi  =>  a^2 >= aa (1 - u) >= Yhi (1 - 2^-18), so with
+//     t_hi, eps2 and eta_hi all scaled by (1 + 2^-17) a^2 is still strictly
+//     above the unscaled Yhi, the strict outlier bound of the proof above.
+// k_score_mf and the VALU decisions stay valid under the slightly wider band.
+constexpr double kMfFoldLo = 1.0 - 0x1p-18;
+constexpr double kMfFoldHi = 1.0 + 0x1p-17;
 constexpr double kMfDelta = 1.0 / (double)(1 << SFM_MF_AMGM);
 constexpr double kMfPin = 1.0 + (double)(1 << SFM_MF_AMGM);    // 1 + 1/delta
 constexpr double kMfPout = (double)(1 << SFM_MF_AMGM);         // 1/delta
@@ -125,8 +143,8 @@ __host__ inline bool mf_params(double thr, MfParams* p) {
   while (k < 15 && std::ldexp(thr, k + 1) <= 1.0) ++k;          // 2^k <= 1/thr < 2^(k+1)
   const double t = std::ldexp(thr * thr, 2 * k);                 // in (0.25, 1]
   p->k = k;
-  p->t_lo = t * (1.0 - 0x1p-40) * (1.0 - 0x1p-22) * (1.0 - 0x1p-18) / (1.0 + kMfDelta);
-  p->t_hi = t * (1.0 + 0x1p-40) * (1.0 + 0x1p-22) * (1.0 + 0x1p-18) / (1.0 - kMfDelta);
+  p->t_lo = t * (1.0 - 0x1p-40) * (1.0 - 0x1p-22) * (1.0 - 0x1p-18) * kMfFoldLo / (1.0 + kMfDelta);
+  p->t_hi = t * (1.0 + 0x1p-40) * (1.0 + 0x1p-22) * (1.0 + 0x1p-18) * kMfFoldHi / (1.0 - kMfDelta);
   return true;
 }
 
@@ -227,9 +245,9 @@ __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, con
     const double e1s1 = 16.0 * infl * kMfPin * K1 * K1 / (1.0 + kMfDelta);     // x (s1/4)^2
     const double e1s2 = 16.0 * infl * kMfPin * K2 * K2 / (1.0 + kMfDelta);
     const double e1c = infl * kMfPin * K3 * K3 / (1.0 + kMfDelta);
-    const double e2s1 = 16.0 * infl * kMfPout * K1 * K1 / (1.0 - kMfDelta);
-    const double e2s2 = 16.0 * infl * kMfPout * K2 * K2 / (1.0 - kMfDelta);
-    const double e2c = infl * kMfPout * K3 * K3 / (1.0 - kMfDelta);
+    const double e2s1 = 16.0 * infl * kMfPout * K1 * K1 / (1.0 - kMfDelta) * kMfFoldHi;
+    const double e2s2 = 16.0 * infl * kMfPout * K2 * K2 / (1.0 - kMfDelta) * kMfFoldHi;
+    const double e2c = infl * kMfPout * K3 * K3 / (1.0 - kMfDelta) * kMfFoldHi;
     // the constant monomial carries g_2 -/+ eps (its f16 rounding is covered by eta)
     row[32 + 2] = (_Float16)(float)(mp.t_lo * g[2] - e1c);
     row[48 + 2] = (_Float16)(float)(mp.t_hi * g[2] + e2c);
@@ -243,7 +261,7 @@ __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, con
     // eta: f16 coefficients and monomials (2^-11 relative each; 2^-25 absolute
     // when subnormal, on either side) and the accumulation, per M^2 (M >= 1)
     const double eta_lo = (1.048e-3 * sl + 11.0 * 0x1p-25 * (ml + 1.0)) * (1.0 + 0x1p-9);
-    const double eta_hi = (1.048e-3 * sh + 11.0 * 0x1p-25 * (mh + 1.0)) * (1.0 + 0x1p-9);
+    const double eta_hi = (1.048e-3 * sh + 11.0 * 0x1p-25 * (mh + 1.0)) * (1.0 + 0x1p-9) * kMfFoldHi;
     const _Float16 Blo = f16_up(eta_lo), Bhi = f16_up(eta_hi);
     const _Float16 S1lo = f16_up(e1s1), S2lo = f16_up(e1s2), S1hi = f16_up(e2s1), S2hi = f16_up(e2s2);
     if (isfinite((float)Blo) && isfinite((float)Bhi) && isfinite((float)S1lo) && isfinite((float)S2lo) &&

@@ -45,6 +45,9 @@
 #ifndef SFM_MF2_CARRY
 #define SFM_MF2_CARRY 0
 #endif
+#ifndef SFM_MF2_FOLD
+#define SFM_MF2_FOLD 1
+#endif
 constexpr int kMf2Waves = SFM_MF2_WAVES;       // 12: 3 per SIMD, two accumulator sets; 16: 4 per SIMD, one
 constexpr int kMf2Wpe = kMf2Waves / 4;
 constexpr int kMf2Span = SFM_MF2_SPAN;         // points per staged span
@@ -116,6 +119,59 @@ __device__ __forceinline__ void mf2_decide(const MfAcc& r, uint32_t (&s1)[16], u
     __builtin_amdgcn_sched_barrier(0);
 #endif
   }
+}
+
+// SFM_MF2_FOLD (12-wave build): a^2 folded into the band MFMAs (the bound:
+// score_mf.h, kMfFoldLo / kMfFoldHi).  Per tile a = two MFMAs as before, then
+// aa = a * a (16 VALU) becomes the C operand of z1 = aa - Ylo and z2 = aa - Yhi
+// (the A rows of Ylo / Yhi negated once per run), and the decisions are the
+// two sign bits alone: 48 VALU per tile instead of 64 (the two FMAs per
+// evaluation become one multiply).  s1 holds inlier bits (z1 < 0) as before;
+// s2 holds NOT-outlier bits (z2 < 0), so undecided = s2 & ~s1.
+// Pipelined over three tiles: tile t+1's a MFMAs, tile t's aa and z MFMAs and
+// tile t-1's sign bits in one step.
+struct MfAB {                                                 // a fragments of one tile (ds_read_b128 x 2)
+  mf_half8 b1, b2;
+};
+__device__ __forceinline__ MfAB mf2_load_ab(const _Float16* frag_tile, int lane) {
+  MfAB b;
+  b.b1 = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(0 * 64 + lane) * 8);
+  b.b2 = *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(1 * 64 + lane) * 8);
+  return b;
+}
+__device__ __forceinline__ mf_half8 mf2_load_d(const _Float16* frag_tile, int lane) {
+  return *reinterpret_cast<const mf_half8*>(frag_tile + (size_t)(2 * 64 + lane) * 8);
+}
+__device__ __forceinline__ mf_float16 mf2_a(const MfAB& B, mf_half8 A1, mf_half8 A2) {
+  mf_float16 z;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) z[g] = 0.0f;
+  const mf_float16 a = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B.b1, z, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(A2, B.b2, a, 0, 0, 0);
+}
+struct MfZ {
+  mf_float16 z1, z2;
+};
+__device__ __forceinline__ MfZ mf2_z(mf_half8 bd, mf_half8 NL, mf_half8 NH, const mf_float16& a) {
+  mf_float16 aa;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) aa[g] = a[g] * a[g];
+  MfZ r;
+  r.z1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(NL, bd, aa, 0, 0, 0);
+  r.z2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(NH, bd, aa, 0, 0, 0);
+  return r;
+}
+__device__ __forceinline__ void mf2_signs(const MfZ& r, uint32_t (&s1)[16], uint32_t (&s2)[16]) {
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    s1[g] = __builtin_amdgcn_alignbit(s1[g], __float_as_uint(r.z1[g]), 31);
+    s2[g] = __builtin_amdgcn_alignbit(s2[g], __float_as_uint(r.z2[g]), 31);
+  }
+}
+constexpr bool kMf2Fold = SFM_MF2_FOLD && kMf2Waves == 12;
+// undecided evaluations of a decision-string pair
+__device__ __forceinline__ uint32_t mf2_undecided(uint32_t s1, uint32_t s2) {
+  return kMf2Fold ? (s2 & ~s1) : ~(s1 | s2);
 }
 
 // the lane id, recomputed where it is used (v_mbcnt) instead of kept live
@@ -268,6 +324,28 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           mf2_decide(r, s1, s2);
         }
 #else
+        if (kMf2Fold) {
+          // step t: a(t+1) MFMAs, aa(t) -> z(t) MFMAs, sign bits of z(t-1)
+          // (step 0 and the last step peeled; pairs of steps ping-pong the
+          // a / z register sets)
+          const mf_half8 NL = -AL, NH = -AH;
+          mf_float16 aA = mf2_a(mf2_load_ab(fr, mf2_lane()), A1, A2), aB;
+          MfZ zA, zB;
+          aB = mf2_a(mf2_load_ab(fr + (size_t)1 * kTileHalves, mf2_lane()), A1, A2);
+          zA = mf2_z(mf2_load_d(fr, mf2_lane()), NL, NH, aA);
+#pragma unroll 1
+          for (int t = 1; t < kMf2Tiles - 1; t += 2) {
+            aA = mf2_a(mf2_load_ab(fr + (size_t)(t + 1) * kTileHalves, mf2_lane()), A1, A2);
+            zB = mf2_z(mf2_load_d(fr + (size_t)t * kTileHalves, mf2_lane()), NL, NH, aB);
+            mf2_signs(zA, s1, s2);
+            aB = mf2_a(mf2_load_ab(fr + (size_t)(t + 2) * kTileHalves, mf2_lane()), A1, A2);
+            zA = mf2_z(mf2_load_d(fr + (size_t)(t + 1) * kTileHalves, mf2_lane()), NL, NH, aA);
+            mf2_signs(zB, s1, s2);
+          }
+          zB = mf2_z(mf2_load_d(fr + (size_t)(kMf2Tiles - 1) * kTileHalves, mf2_lane()), NL, NH, aB);
+          mf2_signs(zA, s1, s2);
+          mf2_signs(zB, s1, s2);
+        } else {
         // two accumulator sets: tile t+1's MFMAs beside tile t's decisions
         // (the last pair peeled, so the loop body has no conditional MFMA)
         MfB B = mf_load_b(fr, mf2_lane());
@@ -285,6 +363,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         rb = mf_tile_mfma(B, A1, A2, AL, AH);
         mf2_decide(ra, s1, s2);
         mf2_decide(rb, s1, s2);
+        }
 #endif
       }
       MF_STAMP(1);
@@ -301,7 +380,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       // is tile kMf2Tiles-1-j, point 32 (kMf2Tiles-1-j) + rl of the span.
       int nl = 0;
 #pragma unroll
-      for (int g = 0; g < 16; ++g) nl += __popc(~(s1[g] | s2[g]));
+      for (int g = 0; g < 16; ++g) nl += __popc(mf2_undecided(s1[g], s2[g]));
       const int incl = mf_wave_scan(nl, lane);
       const int qtotal = __builtin_amdgcn_readlane(incl, 63);
 #ifdef SFM_MF_STATS
@@ -315,7 +394,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         uint32_t* q = queue + qn + (incl - nl);
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-          uint32_t uu = ~(s1[g] | s2[g]);
+          uint32_t uu = mf2_undecided(s1[g], s2[g]);
           const uint32_t top = ((uint32_t)k << 15) | ((uint32_t)mf_row(g, hl) << 10) |
                                (uint32_t)(32 * (kMf2Tiles - 1) + rl);
           while (uu) {
@@ -346,7 +425,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           int pos = incl - nl - base;
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
-            uint32_t uu = ~(s1[g] | s2[g]);
+            uint32_t uu = mf2_undecided(s1[g], s2[g]);
             const uint32_t top = ((uint32_t)k << 15) | ((uint32_t)mf_row(g, hl) << 10) |
                                  (uint32_t)(32 * (kMf2Tiles - 1) + rl);
             while (uu) {
@@ -370,7 +449,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           uint32_t* q = queue + pos;
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
-            uint32_t uu = ~(s1[g] | s2[g]);
+            uint32_t uu = mf2_undecided(s1[g], s2[g]);
             const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
             while (uu) {
               *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
@@ -380,7 +459,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         } else {
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
-            uint32_t uu = ~(s1[g] | s2[g]);
+            uint32_t uu = mf2_undecided(s1[g], s2[g]);
             const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
             while (uu) {
               if (pos >= 0 && pos < kMf2Queue) queue[pos] = top - 32u * (uint32_t)__builtin_ctz(uu);
