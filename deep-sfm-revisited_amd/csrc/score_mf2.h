@@ -19,10 +19,12 @@
 //   * Logical block ranges are contiguous per XCD (block id % 8 picks the
 //     XCD), so an XCD's blocks work on one or two pairs and that pair's A
 //     rows (1.3 MB) and E rows stay in its L2.
-//   * The tile loop runs two accumulator sets: tile t+1's four MFMAs issue
-//     before tile t's 64 decision VALU, so one wave keeps the matrix pipe and
-//     the vector issue busy together (scripts/probe_tile.hip: 247 -> 213 SIMD
-//     cycles per tile at 3 waves per SIMD).  Spans are 32 tiles: the 32-bit
+//   * The tile loop keeps the matrix pipe and the vector issue busy together
+//     from one wave: round 2's decisions ran two accumulator sets (tile t+1's
+//     four MFMAs before tile t's 64 decision VALU; scripts/probe_tile.hip: 247
+//     -> 213 SIMD cycles per tile at 3 waves per SIMD); the folded decisions
+//     (SFM_MF2_FOLD, default) pipeline a / aa+z / signs over three tiles with
+//     48 decision VALU per tile.  Spans are 32 tiles: the 32-bit
 //     decision strings are full, and a run's fixed costs (A rows, queue,
 //     float64 drain, count reduction) spread over 32 tiles instead of 24.
 //   * The next run's A rows load right after the tile loop, under the
@@ -168,7 +170,7 @@ __device__ __forceinline__ void mf2_signs(const MfZ& r, uint32_t (&s1)[16], uint
     s2[g] = __builtin_amdgcn_alignbit(s2[g], __float_as_uint(r.z2[g]), 31);
   }
 }
-constexpr bool kMf2Fold = SFM_MF2_FOLD && kMf2Waves == 12;
+constexpr bool kMf2Fold = SFM_MF2_FOLD;
 // undecided evaluations of a decision-string pair
 __device__ __forceinline__ uint32_t mf2_undecided(uint32_t s1, uint32_t s2) {
   return kMf2Fold ? (s2 & ~s1) : ~(s1 | s2);
@@ -315,6 +317,17 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #if SFM_MF2_WAVES > 12
         // four waves per SIMD (128 VGPRs): one accumulator set, the B
         // fragments one tile ahead; the other waves cover the MFMA latency
+        if (kMf2Fold) {
+          // one register set; the other three waves of the SIMD cover the
+          // a -> aa -> z -> signs dependency chain
+          const mf_half8 NL = -AL, NH = -AH;
+#pragma unroll 1
+          for (int t = 0; t < kMf2Tiles; ++t) {
+            const mf_float16 a = mf2_a(mf2_load_ab(fr + (size_t)t * kTileHalves, mf2_lane()), A1, A2);
+            const MfZ z = mf2_z(mf2_load_d(fr + (size_t)t * kTileHalves, mf2_lane()), NL, NH, a);
+            mf2_signs(z, s1, s2);
+          }
+        } else {
         MfB bn = mf_load_b(fr, mf2_lane());
 #pragma unroll 1
         for (int t = 0; t < kMf2Tiles; ++t) {
@@ -322,6 +335,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           if (t + 1 < kMf2Tiles) bn = mf_load_b(fr + (size_t)(t + 1) * kTileHalves, mf2_lane());
           const MfAcc r = mf_tile_mfma(bc, A1, A2, AL, AH);
           mf2_decide(r, s1, s2);
+        }
         }
 #else
         if (kMf2Fold) {
