@@ -50,6 +50,9 @@
 #ifndef SFM_MF2_FOLD
 #define SFM_MF2_FOLD 1
 #endif
+#ifndef SFM_MF2_BPRE
+#define SFM_MF2_BPRE 0
+#endif
 constexpr int kMf2Waves = SFM_MF2_WAVES;       // 12: 3 per SIMD, two accumulator sets; 16: 4 per SIMD, one
 constexpr int kMf2Wpe = kMf2Waves / 4;
 constexpr int kMf2Span = SFM_MF2_SPAN;         // points per staged span
@@ -343,6 +346,37 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           // (step 0 and the last step peeled; pairs of steps ping-pong the
           // a / z register sets)
           const mf_half8 NL = -AL, NH = -AH;
+#if SFM_MF2_BPRE
+          // B fragments one step ahead (12 more VGPRs: the 8-wave build)
+          auto ldab = [&](int t) { return mf2_load_ab(fr + (size_t)min(t, kMf2Tiles - 1) * kTileHalves, mf2_lane()); };
+          auto ldd = [&](int t) { return mf2_load_d(fr + (size_t)min(t, kMf2Tiles - 1) * kTileHalves, mf2_lane()); };
+          MfAB ab1 = ldab(1);
+          mf_half8 d0 = ldd(0);
+          mf_float16 aA = mf2_a(ldab(0), A1, A2), aB;
+          MfZ zA, zB;
+          aB = mf2_a(ab1, A1, A2);
+          ab1 = ldab(2);
+          zA = mf2_z(d0, NL, NH, aA);
+          d0 = ldd(1);
+#pragma unroll 1
+          for (int t = 1; t < kMf2Tiles - 1; t += 2) {
+            aA = mf2_a(ab1, A1, A2);                      // a(t + 1)
+            ab1 = ldab(t + 2);
+            zB = mf2_z(d0, NL, NH, aB);                   // z(t)
+            d0 = ldd(t + 1);
+            mf2_signs(zA, s1, s2);                        // t - 1
+            aB = mf2_a(ab1, A1, A2);                      // a(t + 2)
+            ab1 = ldab(t + 3);
+            zA = mf2_z(d0, NL, NH, aA);                   // z(t + 1)
+            d0 = ldd(t + 2);
+            mf2_signs(zB, s1, s2);                        // t
+          }
+          zB = mf2_z(d0, NL, NH, aB);
+          mf2_signs(zA, s1, s2);
+          mf2_signs(zB, s1, s2);
+        } else if (kMf2Fold) {
+          const mf_half8 NL = -AL, NH = -AH;
+#endif
           mf_float16 aA = mf2_a(mf2_load_ab(fr, mf2_lane()), A1, A2), aB;
           MfZ zA, zB;
           aB = mf2_a(mf2_load_ab(fr + (size_t)1 * kTileHalves, mf2_lane()), A1, A2);
