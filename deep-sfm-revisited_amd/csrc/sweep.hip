@@ -843,7 +843,12 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
         f32x4 t[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
+#ifdef SFM_SWEEP_EXP_NOGATHER
+          // experiment builds only (what binds the sweep): no tap gathers
+          t[e] = f32x4{tp.wt[e], tp.wt[e] + 1.0f, __uint_as_float(tp.off[e]), (float)n};
+#else
           t[e] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtq, tp.off[e] * 16u, so, 0));
+#endif
         f32x4 a;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
