@@ -834,7 +834,12 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
         }
         if (in) acc[n][j] = a;
       }
+#ifdef SFM_SWEEP_EXP_NOSAMPLE
+    // experiment builds only: the sample at the pixel itself (no projection)
+    } else if ((ix = xf + 0.25f * d * 1e-9f, iy = yf, true)) {
+#else
     } else if (sample_pos_nr(pr, ray, d, sk, ix, iy)) {
+#endif
       TapsIn tp;
       make_taps_inside(ix, iy, g.h, g.w, tp);
 #pragma unroll
