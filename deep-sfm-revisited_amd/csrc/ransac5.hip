@@ -420,9 +420,13 @@ __device__ __forceinline__ void fp32_constants(const double* E, double thr, bool
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kChains) void k_chain(int H, int iters, const int32_t* __restrict__ nroots,
                                                    const int32_t* __restrict__ ncand, int32_t* __restrict__ cand_off,
-                                                   int32_t* __restrict__ chain_ref, int32_t* __restrict__ cand_total) {
+                                                   int32_t* __restrict__ chain_ref, int32_t* __restrict__ cand_total,
+                                                   unsigned long long* __restrict__ skipped) {
   __shared__ int32_t s_sum[kChains / 64];
   const int b = blockIdx.x, t = threadIdx.x;
+  // the call's pruning counter (first chunk only; it accumulates over chunks),
+  // zeroed here rather than by a memset launch of its own
+  if (skipped && b == 0 && t == 0) *skipped = 0ull;
   const size_t hb0 = (size_t)b * H + (size_t)t * iters;
   int cnt = 0;
   for (int i = 0; i < iters; ++i) {
@@ -464,7 +468,8 @@ __global__ __launch_bounds__(256) void k_cand(int H, int iters, int cheir, const
                                               const int32_t* __restrict__ ncand, const double* __restrict__ hypE,
                                               const double* __restrict__ hypP, double* __restrict__ hypP0,
                                               const int32_t* __restrict__ cand_off, double* __restrict__ candE,
-                                              int cmax, double guard_g, double thr, int fast32) {
+                                              int cmax, double guard_g, double thr, int fast32,
+                                              int32_t* __restrict__ cntT, int32_t* __restrict__ cntR) {
   const int b = blockIdx.y;
   const int g = blockIdx.x * 256 + threadIdx.x;
   const int h = g / kMaxSlots, j = g - h * kMaxSlots;
@@ -473,7 +478,12 @@ __global__ __launch_bounds__(256) void k_cand(int H, int iters, int cheir, const
   const size_t hb = hb0 + h;
   const int nc = ncand[hb];
   if (j >= (nc > 0 ? nc : 1)) return;
-  double* dst = candE + ((size_t)b * cmax + cand_off[hb] + j) * kCandStride;
+  const size_t ci = (size_t)b * cmax + cand_off[hb] + j;
+  double* dst = candE + ci * kCandStride;
+  // the scorers add into the counts of candidates < cand_total only: zeroing
+  // them with their records replaces two memset launches per call
+  cntT[ci] = 0;
+  cntR[ci] = 0;
   if (nc > 0) {
     const double* Eh = hypE + (hb * kMaxSlots + j) * 9;
 #pragma unroll
@@ -1723,7 +1733,7 @@ template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
                      const Workspace& w, int ws_batch, double* E_out, double* P_out, int32_t* inliers_out,
-                     int32_t* winner_out, int32_t* score_out, hipStream_t s) {
+                     int32_t* winner_out, int32_t* score_out, hipStream_t s, bool first_chunk) {
   const int H = kChains * iters;
   const int cmax = H * kMaxSlots;
   PairParams pp{};
@@ -1760,13 +1770,12 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   {
     ProfScope ps("ransac_chain", s);
     hipLaunchKernelGGL(k_chain, dim3(bc), dim3(kChains), 0, s, H, iters, w.nroots, w.ncand, w.cand_off, w.chain_ref,
-                       w.cand_total);
+                       w.cand_total, first_chunk ? w.skipped : nullptr);
     hipLaunchKernelGGL(k_cand, dim3((H * kMaxSlots + 255) / 256, bc), dim3(256), 0, s, H, iters, cheir, w.chain_ref,
-                       w.ncand, w.hypE, w.hypP, w.hypP0, w.cand_off, w.candE, cmax, guard_g, thr, fast32 ? 1 : 0);
+                       w.ncand, w.hypE, w.hypP, w.hypP0, w.cand_off, w.candE, cmax, guard_g, thr, fast32 ? 1 : 0,
+                       w.cntT, w.cntR);
   }
   SFM_LAUNCHED();
-  SFM_HIP(hipMemsetAsync(w.cntT, 0, (size_t)bc * cmax * 4, s));
-  SFM_HIP(hipMemsetAsync(w.cntR, 0, (size_t)bc * cmax * 4, s));
   ScoreConsts kc;
   kc.thr = thr;
   kc.t2lo = (thr * thr) * (1.0 - 0x1p-22);
@@ -1826,14 +1835,13 @@ static int run_src(const Src& src, const int64_t* n, int batch, int num_test, in
   }
   Workspace w;
   layout((char*)ws, bc, 0, iters, &w);
-  SFM_HIP(hipMemsetAsync(w.skipped, 0, 8, s));
   const int H = kChains * iters;
   for (int b0 = 0; b0 < batch; b0 += bc) {
     const int nb = std::min(bc, batch - b0);
     if (int rc = run_chunk(src.shifted(b0), n + b0, nb, num_test, num_ransac_test, iters, thr, seed, cheir, w, bc,
                            E_out + (size_t)b0 * 9, P_out ? P_out + (size_t)b0 * 12 : nullptr, inliers_out + b0,
                            winner_out ? winner_out + b0 : nullptr,
-                           score_out ? score_out + (size_t)b0 * H : nullptr, s))
+                           score_out ? score_out + (size_t)b0 * H : nullptr, s, b0 == 0))
       return rc;
   }
   return SFM_OK;
