@@ -185,8 +185,8 @@ int sfm_plane_sweep_correlation(const float* ref, const float* tgt, int batch, i
                                 int depth_mode, float* cost, void* workspace, size_t workspace_bytes,
                                 void* stream) {
   SFM_REQUIRE(ref && tgt && pose && K4 && K4inv && cost, "null pointer argument");
-  SFM_REQUIRE(batch >= 1 && batch <= 65535 && channels >= 1 && h >= 2 && w >= 2 && nlabel >= 1,
-              "invalid correlation shape");
+  SFM_REQUIRE(batch >= 1 && batch <= 65535 && channels >= 1 && channels <= 4 * 65535 && h >= 2 && w >= 2 &&
+              nlabel >= 1, "invalid correlation shape");
   SFM_REQUIRE(depth_mode == 0 || depth_mode == 1, "depth_mode must be 0 (inverse depth) or 1 (depth)");
   SFM_REQUIRE(min_depth > 0.0f, "min_depth must be positive");
   SFM_REQUIRE((int64_t)h * w < ((int64_t)1 << 30), "feature map too large");

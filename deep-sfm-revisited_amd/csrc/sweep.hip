@@ -47,6 +47,43 @@ __device__ __forceinline__ float plane_depth(float dmax, float dstep, int l) {
   return dstep > 0.0f ? (float)(l + 1) * dstep : dmax / (float)(l + 1);
 }
 
+// The tensor preparation of PSNet.forward before its sweep loop, one thread per
+// pair (run by k_tgt_quads, before that pair's Proj), in the reference's float32 operations (PSNet.py:130-133 and the
+// RESCALE_DEPTH branch): P.float() (RNE from float64), translation * t_scale,
+// K rows 0-1 / 4, K^-1[:2,:2] * 4.  Division by 4 and multiplication by 4
+// are exact, and the conversion and the one multiply are correctly rounded,
+// so the results equal the torch ops bit for bit.
+struct PsnetPrep {          // sfm_plane_sweep_psnet's inputs (PSNet.py:130-133 + RESCALE_DEPTH)
+  const void* pose;
+  int pose_f64;
+  const float* K;
+  const float* Kinv;
+  float t_scale;
+  float* out;               // planar: B poses (12), then B K4 (9), then B K4inv (9)
+};
+
+// one pair's preparation into P[12], K4[9], Ki4[9] (registers), also stored
+// to the workspace for the sweep kernels that read them from there
+__device__ __forceinline__ void psnet_prep_pair(const PsnetPrep& q, int B, int b, float (&P)[12], float (&K4)[9],
+                                                float (&Ki4)[9]) {
+#pragma unroll
+  for (int e = 0; e < 12; ++e) {
+    float v = q.pose_f64 ? (float)static_cast<const double*>(q.pose)[(size_t)b * 12 + e]
+                         : static_cast<const float*>(q.pose)[(size_t)b * 12 + e];
+    if (q.t_scale > 0.0f && (e & 3) == 3) v = v * q.t_scale;
+    P[e] = v;
+    q.out[(size_t)b * 12 + e] = v;
+  }
+#pragma unroll
+  for (int e = 0; e < 9; ++e) {
+    const float k = q.K[(size_t)b * 9 + e], ki = q.Kinv[(size_t)b * 9 + e];
+    K4[e] = e < 6 ? k / 4.0f : k;
+    Ki4[e] = (e == 0 || e == 1 || e == 3 || e == 4) ? ki * 4.0f : ki;
+    q.out[(size_t)B * 12 + (size_t)b * 9 + e] = K4[e];
+    q.out[(size_t)B * 21 + (size_t)b * 9 + e] = Ki4[e];
+  }
+}
+
 // tgt [B][C][hw] -> tq [B][C4][hw] float4 (channels >= C are zero).  With
 // `projs`, threads 0..B-1 also write each pair's Proj (K.pose rows and K^-1,
 // load_proj's float32 expression order), so the sweep's waves read it with
@@ -56,33 +93,45 @@ __device__ __forceinline__ float plane_depth(float dmax, float dstep, int l) {
 __global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4, int hw, f32x4* __restrict__ tq,
                             const float* __restrict__ pose, const float* __restrict__ K4,
                             const float* __restrict__ K4inv, Proj* __restrict__ projs, int L, float dmax,
-                            float dstep, float* __restrict__ depths) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)B * C4 * hw;
-  if (projs && i < B) {
-    Proj pr;
-    load_proj(pose, K4, K4inv, (int)i, pr);
-    projs[i] = pr;
+                            float dstep, float* __restrict__ depths, PsnetPrep prep) {
+  // grid (pixels, quads, pairs): no integer division per thread; the uniform
+  // per-pair and per-plane tables from the first quad row of pair 0
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int q = (int)blockIdx.y, b = (int)blockIdx.z;
+  if (q == 0 && b == 0) {
+    if (projs && i < B) {
+      // sfm_plane_sweep_psnet: the pair's PSNet preparation first (the sweep's
+      // other paths read it from the workspace), then its Proj from those values
+      Proj pr;
+      if (prep.out) {
+        float P[12], Kq[9], Kqi[9];
+        psnet_prep_pair(prep, B, i, P, Kq, Kqi);
+        load_proj(P, Kq, Kqi, 0, pr);
+      } else {
+        load_proj(pose, K4, K4inv, i, pr);
+      }
+      projs[i] = pr;
+    }
+    if (depths && i < L) depths[i] = plane_depth(dmax, dstep, i);
   }
-  if (depths && i < L) depths[i] = plane_depth(dmax, dstep, (int)i);
-  if (i >= total) return;
-  const int p = (int)(i % hw);
-  const int64_t bq = i / hw;
-  const int q = (int)(bq % C4), b = (int)(bq / C4);
+  if (i >= hw) return;
   f32x4 v;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int c = 4 * q + k;
-    v[k] = c < C ? tgt[((size_t)b * C + c) * hw + p] : 0.0f;
+    v[k] = c < C ? tgt[((size_t)b * C + c) * hw + i] : 0.0f;
   }
-  tq[i] = v;
+  tq[((size_t)b * C4 + q) * hw + i] = v;
+}
+
+static dim3 quads_grid(int B, int C4, int hw, int extra) {
+  return dim3((unsigned)((std::max(hw, extra) + 255) / 256), (unsigned)C4, (unsigned)B);
 }
 
 void launch_channel_quads(const float* feat, int B, int C, int hw, f32x4* quads, hipStream_t s) {
   const int C4 = (C + 3) / 4;
-  const int64_t n = (int64_t)B * C4 * hw;
-  hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, feat, B, C, C4, hw, quads,
-                     nullptr, nullptr, nullptr, nullptr, 0, 0.0f, 0.0f, nullptr);
+  hipLaunchKernelGGL(k_tgt_quads, quads_grid(B, C4, hw, 0), dim3(256), 0, s, feat, B, C, C4, hw, quads,
+                     nullptr, nullptr, nullptr, nullptr, 0, 0.0f, 0.0f, nullptr, PsnetPrep{});
 }
 
 __device__ __forceinline__ void store4(float* dst, const float (&v)[4]) {
@@ -1286,39 +1335,13 @@ static size_t sweep_core_bytes(int B, int C, int h, int w) {
 // the public size: the core plus the sfm_plane_sweep_psnet operands at its end
 static size_t sweep_ws_bytes(int B, int C, int h, int w) { return sweep_core_bytes(B, C, h, w) + sweep_psnet_bytes(B); }
 
-// The tensor preparation of PSNet.forward before its sweep loop, one thread per
-// pair, in the reference's float32 operations (PSNet.py:130-133 and the
-// RESCALE_DEPTH branch): P.float() (RNE from float64), translation * t_scale,
-// K rows 0-1 / 4, K^-1[:2,:2] * 4.  Division by 4 and multiplication by 4
-// are exact, and the conversion and the one multiply are correctly rounded,
-// so the results equal the torch ops bit for bit.
-__global__ void k_psnet_prep(int B, const void* __restrict__ pose, int pose_f64, const float* __restrict__ K,
-                             const float* __restrict__ Kinv, float t_scale, float* __restrict__ out) {
-  const int b = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (b >= B) return;
-  float* P = out + (size_t)b * 12;                       // planar: poses, then K4, then K4inv
-  float* K4 = out + (size_t)B * 12 + (size_t)b * 9;
-  float* Ki4 = out + (size_t)B * 21 + (size_t)b * 9;
-#pragma unroll
-  for (int e = 0; e < 12; ++e) {
-    float v = pose_f64 ? (float)static_cast<const double*>(pose)[(size_t)b * 12 + e]
-                       : static_cast<const float*>(pose)[(size_t)b * 12 + e];
-    if (t_scale > 0.0f && (e & 3) == 3) v = v * t_scale;
-    P[e] = v;
-  }
-#pragma unroll
-  for (int e = 0; e < 9; ++e) {
-    const float k = K[(size_t)b * 9 + e], ki = Kinv[(size_t)b * 9 + e];
-    K4[e] = e < 6 ? k / 4.0f : k;
-    Ki4[e] = (e == 0 || e == 1 || e == 3 || e == 4) ? ki * 4.0f : ki;
-  }
-}
-
 static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B, int C, int h, int w,
                         const float* pose, const float* K4, const float* K4inv, int L, float min_depth,
-                        int depth_mode, int out_dtype, void* out, void* ws, size_t ws_bytes, hipStream_t s) {
+                        int depth_mode, int out_dtype, void* out, void* ws, size_t ws_bytes, hipStream_t s,
+                        const PsnetPrep& prep = PsnetPrep{}) {
   SFM_REQUIRE(tgt && pose && K4 && K4inv && out && (!with_ref || ref), "null pointer argument");
-  SFM_REQUIRE(B >= 1 && C >= 1 && h >= 2 && w >= 2 && L >= 1, "invalid sweep shape");
+  SFM_REQUIRE(B >= 1 && B <= 65535 && C >= 1 && C <= 4 * 65535 && h >= 2 && w >= 2 && L >= 1,
+              "invalid sweep shape");   // k_tgt_quads' grid: quads in y, pairs in z
   SFM_REQUIRE(out_dtype == 0 || out_dtype == 1, "out_dtype must be 0 (float32) or 1 (bfloat16)");
   SFM_REQUIRE(depth_mode == 0 || depth_mode == 1, "depth_mode must be 0 (inverse depth) or 1 (depth)");
   SFM_REQUIRE(min_depth > 0.0f, "min_depth must be positive");
@@ -1351,10 +1374,8 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   float* depths = L <= kDepthTable ? reinterpret_cast<float*>((char*)projs + sweep_proj_bytes(B)) : nullptr;
   {
     ProfScope ps("sweep_tgt_quads", s);
-    const int64_t nq4 = (int64_t)B * g.C4 * hw;
-    const int64_t nthr = std::max(nq4, (int64_t)std::max(B, L));
-    hipLaunchKernelGGL(k_tgt_quads, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, tgt, B, C, g.C4, hw, tq,
-                       pose, K4, K4inv, projs, L, g.dmax, g.dstep, depths);
+    hipLaunchKernelGGL(k_tgt_quads, quads_grid(B, g.C4, hw, std::max(B, L)), dim3(256), 0, s, tgt, B, C, g.C4, hw, tq,
+                       pose, K4, K4inv, projs, L, g.dmax, g.dstep, depths, prep);
   }
   SFM_LAUNCHED();
   const char* pname = with_ref ? "plane_sweep" : "plane_sweep_warped";
@@ -1505,13 +1526,13 @@ int sfm_plane_sweep_psnet(const float* ref, const float* tgt, int batch, int cha
   }
   hipStream_t s = (hipStream_t)stream;
   float* prep = reinterpret_cast<float*>((char*)workspace + sweep_core_bytes(batch, channels, h, w));
-  hipLaunchKernelGGL(k_psnet_prep, dim3((unsigned)((batch + 63) / 64)), dim3(64), 0, s, batch, pose, pose_dtype, K,
-                     Kinv, t_scale, prep);
-  SFM_LAUNCHED();
-  // the sweep's own scratch excludes the prep region at the workspace's end
+  // the preparation runs inside the sweep's first kernel (k_tgt_quads, one
+  // thread per pair before its Proj), not as a launch of its own; the sweep's
+  // own scratch excludes the prep region at the workspace's end
   return launch_sweep(ref != nullptr, ref, tgt, batch, channels, h, w, prep, prep + (size_t)batch * 12,
                       prep + (size_t)batch * 21, nlabel, min_depth, depth_mode, out_dtype, cost, workspace,
-                      sweep_core_bytes(batch, channels, h, w), s);
+                      sweep_core_bytes(batch, channels, h, w), s,
+                      PsnetPrep{pose, pose_dtype, K, Kinv, t_scale, prep});
 }
 
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w, const float* pose,

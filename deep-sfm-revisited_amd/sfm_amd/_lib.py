@@ -73,6 +73,7 @@ _SIGS = [
       ctypes.c_float, ctypes.c_float, _c_dp, _c_dp]),
     ("sfm_inverse_warp", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp]),
+    ("sfm_kinv3x3", ctypes.c_int, [_c_dp, ctypes.c_int, _c_dp, _c_dp]),
     ("sfm_flow2depth", ctypes.c_int, [_c_dp, _c_dp, _c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
     ("sfm_conv3_bf16", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,

@@ -16,7 +16,23 @@ reused, so a step launches kernels only (hipGraph-capturable).
 """
 import torch
 
-from . import ransac, sweep
+from . import _lib, ransac, sweep
+
+
+def kinv3x3(K):
+    """K^-1 of [B,3,3] (or [3,3]) CUDA intrinsics, float32: torch.inverse's
+    bits on ROCm in one launch (C ABI sfm_kinv3x3)."""
+    if not K.is_cuda:
+        raise RuntimeError("K must be a CUDA tensor")
+    Kf = K.float().contiguous()
+    if Kf.shape[-2:] != (3, 3):
+        raise RuntimeError(f"K must be [..., 3, 3], got {tuple(K.shape)}")
+    out = torch.empty_like(Kf)
+    n = Kf.numel() // 9
+    with torch.cuda.device(Kf.device):
+        _lib.check(_lib.load().sfm_kinv3x3(_lib.ptr(Kf), n, _lib.ptr(out), _lib.stream_ptr(Kf.device)),
+                   "sfm_kinv3x3")
+    return out
 
 
 class TwoViewHotPath:
@@ -55,9 +71,10 @@ class TwoViewHotPath:
 
     @staticmethod
     def k_inverse(K):
-        """K^-1 without a host sync: linalg.inv_ex is torch.inverse's own LU
-        solve minus the singularity check that blocks on the device."""
-        return torch.linalg.inv_ex(K.float())[0]
+        """K^-1 as SFMnet.forward forms it (torch.inverse, models/SFMnet.py:104):
+        one launch of sfm_kinv3x3, bit for bit torch.linalg.inv_ex's result on
+        ROCm (tests/test_gpu_kinv.py), without a host sync."""
+        return kinv3x3(K)
 
     def pose(self, flow, K, Kinv=None):
         if Kinv is None:

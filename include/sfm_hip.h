@@ -273,6 +273,13 @@ int sfm_plane_sweep_correlation(const float* ref, const float* tgt, int batch, i
 int sfm_depth_head(const float* cost, int batch, int nlabel, int h, int w, int H, int W, int depth_mode,
                    float min_depth, float depth_step, float* depth, void* stream);
 
+/* K^-1 of a batch of 3x3 matrices, as models/SFMnet.py:104 forms it
+ * (intrinsic_inv_gpu = torch.inverse(intrinsic_gpu)): bit for bit what
+ * torch.linalg.inv_ex returns on ROCm (rocsolver getrf + getrs order), in one
+ * launch.  K, Kinv [dev] batch x 3 x 3 float32 row-major.  Singular K gives
+ * inf / NaN entries (torch raises). */
+int sfm_kinv3x3(const float* K, int batch, float* Kinv, void* stream);
+
 /* models/inverse_warp.py:121-153 for an arbitrary depth map:
  *   feat [dev] B x C x h x w; depth [dev] B x h x w; pose [dev] B x 3 x 4;
  *   K, Kinv [dev] B x 3 x 3; out [dev] B x C x h x w (float32). */

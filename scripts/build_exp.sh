@@ -13,7 +13,7 @@ build() {
   local name=$1; shift
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -fPIC -shared \
         -I../../include -Wno-unused-result "$@" -o ../../scripts/exp/libsfm_hip_$name.so \
-        capi.hip ransac5.hip sweep.hip depth.hip irls.hip regularize.hip host_polish.cpp
+        capi.hip ransac5.hip sweep.hip depth.hip irls.hip regularize.hip kinv.hip host_polish.cpp
 }
 if [ $# -eq 0 ]; then
   build STATS -DSFM_SCORE_STATS

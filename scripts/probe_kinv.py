@@ -33,7 +33,7 @@ for name, A in (("intrinsics", K), ("general", G)):
         o = out[m]
         val = (o != want).reshape(n, 9).any(1).sum().item()                 # value mismatches (+0 == -0)
         bits = (o.view(torch.int32) != wb).reshape(n, 9)
-        zs = (bits & (o == want)).sum(0).tolist()                             # entries differing only in a zero's sign
+        zs = (bits & (o == want).reshape(n, 9)).sum(0).tolist()                            # entries differing only in a zero's sign
         print("  mode %d: value mismatches %d, zero-sign-only differences per entry %s" % (m, val, zs), flush=True)
         if bits.any():
             k = int(bits.any(1).nonzero()[0])
