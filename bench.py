@@ -160,6 +160,32 @@ def rocprof_kernel_ms(args, prefixes):
     return (tot if hit == set(prefixes) else None), os.path.relpath(best[1], ROOT)
 
 
+ROOFLINE_REGIONS = ("ransac_score", "plane_sweep")
+ALL_REGIONS = ("flow_to_points", "keypoints_to_points", "ransac_solve", "ransac_chain", "ransac_score",
+               "ransac_select", "plane_sweep")
+
+
+def profiled_pass(stepf, inputs, steps, dev):
+    """Average launch time of every profiled stage over `steps` extra steps
+    with all regions evented (outside the timed region)."""
+    import torch
+    from sfm_amd import _lib
+    torch.cuda.synchronize(dev)
+    _lib.profile_reset()
+    _lib.profile_select(None)
+    _lib.profile_enable(True)
+    for _ in range(steps):
+        stepf(*inputs)
+    torch.cuda.synchronize(dev)
+    _lib.profile_enable(False)
+    kt = {}
+    for name in ALL_REGIONS:
+        ms, n = _lib.profile_read(name)
+        if n:
+            kt[name] = ms / n
+    return kt
+
+
 def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, traffic_src, rocprof=None):
     """Roofline line of the RANSAC scoring kernel.  achieved = the algorithmic
     rate (SURVEY §8d: 50 FLOP per (candidate E, correspondence) evaluation);
@@ -379,7 +405,11 @@ def _main_gpu(args, dist):
     for _ in range(args.warmup):
         stepf(flow, K, ref_fea, tgt_fea)
     torch.cuda.synchronize(dev)
+    # HIP events inside the timed region only around the two roofline kernels:
+    # every evented launch adds two event records to the stream (sparse step
+    # 1.722 -> 1.772 ms with all seven regions evented, scripts/event_ab.py)
     _lib.profile_reset()
+    _lib.profile_select(ROOFLINE_REGIONS)
     _lib.profile_enable(True)
     dist.barrier(dev)
     torch.cuda.synchronize(dev)
@@ -398,11 +428,13 @@ def _main_gpu(args, dist):
     gathered = dist.gather_rows(rows, world).cpu()
 
     kt = {}
-    for name in ("flow_to_points", "keypoints_to_points", "ransac_solve", "ransac_chain", "ransac_score",
-                 "ransac_select", "plane_sweep"):
+    for name in ROOFLINE_REGIONS:
         ms, n = _lib.profile_read(name)
         if n:
             kt[name] = ms / n
+    # the other stages' launch times: a separate, fully evented pass after the
+    # timed region (same inputs and outputs; never part of `value`)
+    kt_all = profiled_pass(stepf, (flow, K, ref_fea, tgt_fea), min(args.steps, 5), dev)
     cands = ransac.candidate_counts(hp.ws, B, args.iters)
     evals = sum(cands) * hp.n                       # candidate E x correspondences per launch
     skipped = ransac.skipped_evaluations(hp.ws, B, args.iters)   # exact bound pruning (last launch)
@@ -452,9 +484,11 @@ def _main_gpu(args, dist):
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,
                                "avg_launch_ms": round(kt["plane_sweep"], 4),
                                "bytes_per_launch": sweep_bytes},
-            "solve": {"hypotheses_per_launch": hyps, "ms": round(kt["ransac_solve"], 4),
-                      "hypotheses_per_s": round(hyps / (kt["ransac_solve"] * 1e-3), 1)},
-            "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+            "solve": {"hypotheses_per_launch": hyps, "ms": round(kt_all["ransac_solve"], 4),
+                      "hypotheses_per_s": round(hyps / (kt_all["ransac_solve"] * 1e-3), 1)},
+            "kernel_ms": {k: round(v, 4) for k, v in kt_all.items()},
+            "kernel_ms_source": (f"HIP events around every stage in a separate pass of {min(args.steps, 5)} steps "
+                                 f"after the timed region; the timed region events only {', '.join(ROOFLINE_REGIONS)}"),
             "inliers": [int(v) for v in gathered[:, 21].tolist()],
             "gathered": {"pairs": int(gathered.shape[0]), "per_rank": [len(dist.shard(world * B, r, world))
                                                                        for r in range(world)],

@@ -1,5 +1,7 @@
 // Error reporting and per-kernel event profiling for libsfm_hip.
+#include <algorithm>
 #include <mutex>
+#include <string>
 #include <vector>
 #include <cstring>
 #include "common.h"
@@ -24,6 +26,7 @@ struct Slot {
 };
 std::mutex g_mu;
 bool g_enabled = false;
+std::vector<std::string> g_select;   // empty: every name is recorded
 std::vector<Slot> g_slots;
 std::vector<hipEvent_t> g_pool;
 
@@ -60,6 +63,7 @@ void drain(Slot& s) {
 ProfScope::ProfScope(const char* name, hipStream_t s) : slot(-1), stream(s) {
   if (!g_enabled) return;
   std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_select.empty() && std::find(g_select.begin(), g_select.end(), name) == g_select.end()) return;
   slot = slot_of(name);
   hipEvent_t a = take_event(), b = take_event();
   if (!a || !b) { slot = -1; return; }
@@ -94,6 +98,7 @@ bool v_1_16(int v) { return v >= 1 && v <= 16; }
 bool v_01(int v) { return v == 0 || v == 1; }
 const TuneKey kTuneKeys[] = {
     {"solve_lanes", &sfm::Tuning::solve_lanes, v_1_16},
+    {"solve_coop", &sfm::Tuning::solve_coop, v_01},
     {"roots_lanes", &sfm::Tuning::roots_lanes, [](int v) { return v >= 1 && v <= 32; }},   // LDS stack columns
     {"roots_split", &sfm::Tuning::roots_split, [](int v) { return v == 0 || v == 1; }},
     {"sweep_lane_pixels", &sfm::Tuning::sweep_lane_pixels, [](int v) { return v >= 0 && v <= 2; }},
@@ -146,6 +151,23 @@ int sfm_tune_get(const char* key, int* value) {
 int sfm_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(sfm::g_mu);
   sfm::g_enabled = on != 0;
+  return SFM_OK;
+}
+
+int sfm_profile_select(const char* names) {
+  std::lock_guard<std::mutex> lk(sfm::g_mu);
+  sfm::g_select.clear();
+  if (!names) return SFM_OK;
+  std::string cur;
+  for (const char* c = names;; ++c) {
+    if (*c == ',' || *c == '\0') {
+      if (!cur.empty()) sfm::g_select.push_back(cur);
+      cur.clear();
+      if (*c == '\0') break;
+    } else {
+      cur += *c;
+    }
+  }
   return SFM_OK;
 }
 

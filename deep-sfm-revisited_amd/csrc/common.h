@@ -12,6 +12,7 @@ void set_error(const std::string& msg);
 // Launch-shape tuning knobs (sfm_tune_set); read by the launchers.
 struct Tuning {
   int solve_lanes = 16;          // active lanes per k_solve_front wave (1..16: LDS records)
+  int solve_coop = 1;            // k_solve_front's reduction on DPP quads (4 lanes per hypothesis); 0: one lane
   int roots_lanes = 32;          // active lanes per k_roots wave (1..32: LDS stack columns)
   int roots_split = 1;           // 1: k_roots_split (falsi tasks shared by the wave's 64 lanes); 0: k_roots
   int sweep_items_per_block = 4; // consecutive (row, plane, window) items per sweep block

@@ -150,9 +150,10 @@ __device__ __forceinline__ void essential_basis(const double q[5][2], const doub
   for (int e = 0; e < 9; ++e) { Eb[e].c[0] = M[5][e]; Eb[e].c[1] = M[6][e]; Eb[e].c[2] = M[7][e]; Eb[e].c[3] = M[8][e]; }
 }
 
-// Constraint equations (EEeqns_5pt, essential_matrix_5pt.cu:428-474)
-__device__ __forceinline__ void build_equations(const Lin Eb[9], Eqs& A) {
-  // trace(E E^T), row-major element order (traceEEt)
+// Constraint equations (EEeqns_5pt, essential_matrix_5pt.cu:428-474), in
+// three parts so that a DPP quad can share them (build_equations_quad):
+// trace(E E^T), row-major element order (traceEEt)
+__device__ __forceinline__ Quad trace_eet(const Lin Eb[9]) {
   Quad tr = qmul(Eb[0], Eb[0]);
 #pragma unroll
   for (int e = 1; e < 9; ++e) {
@@ -160,65 +161,94 @@ __device__ __forceinline__ void build_equations(const Lin Eb[9], Eqs& A) {
 #pragma unroll
     for (int k = 0; k < 10; ++k) tr.c[k] = tr.c[k] + s.c[k];
   }
-  // det(E) by cofactors of column 0 (polydet4)
-  {
-    Cubic d[3];
-    const int rows[3][4] = {{4, 8, 7, 5}, {7, 2, 1, 8}, {1, 5, 4, 2}};  // (a*b - c*d)
-    const int col0[3] = {0, 3, 6};
+  return tr;
+}
+
+// equation 0: det(E) by cofactors of column 0 (polydet4)
+__device__ __forceinline__ void det_equation(const Lin Eb[9], Eqs& A) {
+  Cubic d[3];
+  const int rows[3][4] = {{4, 8, 7, 5}, {7, 2, 1, 8}, {1, 5, 4, 2}};  // (a*b - c*d)
+  const int col0[3] = {0, 3, 6};
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      Quad m1 = qmul(Eb[rows[t][0]], Eb[rows[t][1]]);
-      Quad m2 = qmul(Eb[rows[t][2]], Eb[rows[t][3]]);
-      Quad df;
+  for (int t = 0; t < 3; ++t) {
+    Quad m1 = qmul(Eb[rows[t][0]], Eb[rows[t][1]]);
+    Quad m2 = qmul(Eb[rows[t][2]], Eb[rows[t][3]]);
+    Quad df;
 #pragma unroll
-      for (int k = 0; k < 10; ++k) df.c[k] = m1.c[k] - m2.c[k];
-      d[t] = cmul(df, Eb[col0[t]]);
-    }
-    Cubic det;
-#pragma unroll
-    for (int k = 0; k < 20; ++k) det.c[k] = (d[0].c[k] + d[1].c[k]) + d[2].c[k];
-    put_equation(det, A, 0);
+    for (int k = 0; k < 10; ++k) df.c[k] = m1.c[k] - m2.c[k];
+    d[t] = cmul(df, Eb[col0[t]]);
   }
-  // 2 E E^T E - tr(E E^T) E = 0
-  int eqn = 1;
-  for (int i = 0; i < 3; ++i) {
-    Cubic acc[3];
+  Cubic det;
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+  for (int k = 0; k < 20; ++k) det.c[k] = (d[0].c[k] + d[1].c[k]) + d[2].c[k];
+  put_equation(det, A, 0);
+}
+
+// equations 1 + 3i .. 3 + 3i: row i of 2 E E^T E - tr(E E^T) E = 0, with
+// Ei[p] = Eb[3i + p] (the row's three entries)
+__device__ __forceinline__ void row_equations(const Lin Eb[9], const Lin Ei[3], const Quad& tr, Eqs& A, int i) {
+  Cubic acc[3];
 #pragma unroll
-      for (int k = 0; k < 20; ++k) acc[j].c[k] = 0.0;
+  for (int j = 0; j < 3; ++j)
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      Quad eet;
+    for (int k = 0; k < 20; ++k) acc[j].c[k] = 0.0;
 #pragma unroll
-      for (int k = 0; k < 10; ++k) eet.c[k] = 0.0;
+  for (int q = 0; q < 3; ++q) {
+    Quad eet;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        Quad s = qmul(Eb[3 * i + p], Eb[3 * q + p]);
+    for (int k = 0; k < 10; ++k) eet.c[k] = 0.0;
 #pragma unroll
-        for (int k = 0; k < 10; ++k) eet.c[k] += s.c[k];
-      }
+    for (int p = 0; p < 3; ++p) {
+      Quad s = qmul(Ei[p], Eb[3 * q + p]);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        Cubic s = cmul(eet, Eb[3 * q + j]);
-#pragma unroll
-        for (int k = 0; k < 20; ++k) acc[j].c[k] += s.c[k];
-      }
+      for (int k = 0; k < 10; ++k) eet.c[k] += s.c[k];
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      Cubic t = cmul(tr, Eb[3 * i + j]);
-      Cubic r;
+      Cubic s = cmul(eet, Eb[3 * q + j]);
 #pragma unroll
-      for (int k = 0; k < 20; ++k) r.c[k] = acc[j].c[k] * 2.0 - t.c[k];
-      put_equation(r, A, eqn++);
+      for (int k = 0; k < 20; ++k) acc[j].c[k] += s.c[k];
     }
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    Cubic t = cmul(tr, Ei[j]);
+    Cubic r;
+#pragma unroll
+    for (int k = 0; k < 20; ++k) r.c[k] = acc[j].c[k] * 2.0 - t.c[k];
+    put_equation(r, A, 1 + 3 * i + j);
+  }
+}
+
+__device__ __forceinline__ void build_equations(const Lin Eb[9], Eqs& A) {
+  const Quad tr = trace_eet(Eb);
+  det_equation(Eb, A);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) row_equations(Eb, &Eb[3 * i], tr, A, i);
+}
+
+// The same ten equations from a DPP quad holding the same Eb on every lane:
+// lane 0 writes equation 0, lane s = 1..3 the row i = s - 1 block (its rows
+// selected by value, so every index stays static).  Same operations per
+// equation as build_equations; the caller synchronises before reading A.
+__device__ __forceinline__ void build_equations_quad(const Lin Eb[9], Eqs& A, int s) {
+  if (s == 0) {
+    det_equation(Eb, A);
+  } else {
+    const int i = s - 1;
+    Lin Ei[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) Ei[p].c[c] = i == 0 ? Eb[p].c[c] : i == 1 ? Eb[3 + p].c[c] : Eb[6 + p].c[c];
+    row_equations(Eb, Ei, trace_eet(Eb), A, i);
   }
 }
 
 // Row operation: row[target] -= fac * row[prow] on the non-zero column blocks
 // (sweep_up / sweep_down, essential_matrix_5pt.cu:713-779)
 __device__ __forceinline__ void row_axpy(Eqs& A, int prow, int target, int lim0, double fac) {
+#pragma unroll
   for (int j = 0; j <= lim0; ++j) A.e0[target][j] -= fac * A.e0[prow][j];
 #pragma unroll
   for (int j = 0; j < 6; ++j) A.e1[target][j] -= fac * A.e1[prow][j];
@@ -233,9 +263,11 @@ __device__ __forceinline__ void swap_d(double& a, double& b) { double t = a; a =
 __device__ __forceinline__ void pivot_rows(Eqs& A, int last) {
   double best = fabs(A.e0[last][last]);
   int r = last;
+#pragma unroll
   for (int i = 0; i < last; ++i)
     if (fabs(A.e0[i][last]) > best) { r = i; best = fabs(A.e0[i][last]); }
   if (r == last) return;
+#pragma unroll
   for (int j = 0; j <= last; ++j) swap_d(A.e0[last][j], A.e0[r][j]);
 #pragma unroll
   for (int j = 0; j < 6; ++j) swap_d(A.e1[last][j], A.e1[r][j]);
@@ -244,16 +276,65 @@ __device__ __forceinline__ void pivot_rows(Eqs& A, int last) {
   swap_d(A.e3[last][0], A.e3[r][0]);
 }
 
+// One elimination column of the sweep-up with every index static (the set
+// lives in LDS: dynamic bounds left each row_axpy a loop of dependent LDS
+// round trips, 55 % of k_solve_front's cycles).  The pivot row is read once
+// into registers; rows i < C never write it, so every element sees the same
+// operations in the same order as row_axpy (bit-identical).
+template <int C>
+__device__ __forceinline__ void eliminate_up(Eqs& A) {
+  pivot_rows(A, C);
+  const double pv = A.e0[C][C];
+  double p0[C + 1], p1[6], p2[3];
+#pragma unroll
+  for (int j = 0; j <= C; ++j) p0[j] = A.e0[C][j];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) p1[j] = A.e1[C][j];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) p2[j] = A.e2[C][j];
+  const double p3 = A.e3[C][0];
+#pragma unroll
+  for (int i = 0; i < C; ++i) {
+    const double fac = A.e0[i][C] / pv;
+#pragma unroll
+    for (int j = 0; j <= C; ++j) A.e0[i][j] -= fac * p0[j];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) A.e1[i][j] -= fac * p1[j];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) A.e2[i][j] -= fac * p2[j];
+    A.e3[i][0] -= fac * p3;
+  }
+}
+
+// the last step of reduce_Ematrix: raise the degree to eliminate the x terms
+__device__ __forceinline__ void raise_degree(Eqs& A) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double f = A.e1[i][3 + i] / A.e0[3 + i][3 + i];
+    A.e4[i] = -A.e3[i + 3][0] * f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      A.e3[i][j] -= A.e2[i + 3][j] * f;
+      A.e2[i][j] -= A.e1[i + 3][j] * f;
+      A.e1[i][j] -= A.e0[i + 3][j] * f;
+    }
+  }
+}
+
 // reduce_Ematrix (essential_matrix_5pt.cu:852-900)
 __device__ __forceinline__ void reduce_equations(Eqs& A) {
-  for (int c = 9; c >= 3; --c) {
-    pivot_rows(A, c);
-    const double pv = A.e0[c][c];
-    for (int i = 0; i < c; ++i) row_axpy(A, c, i, c, A.e0[i][c] / pv);
-  }
+  eliminate_up<9>(A);
+  eliminate_up<8>(A);
+  eliminate_up<7>(A);
+  eliminate_up<6>(A);
+  eliminate_up<5>(A);
+  eliminate_up<4>(A);
+  eliminate_up<3>(A);
   // sweep_down on the w^0 block, rows 3 and 4
+#pragma unroll
   for (int r = 3; r <= 4; ++r) {
     const double pv = A.e0[r][r];
+#pragma unroll
     for (int i = r + 1; i <= 5; ++i) row_axpy(A, r, i, r, A.e0[i][r] / pv);
   }
   // sweep_up on the w^1 block: (row 2, col 5) then (row 1, col 4)
@@ -270,18 +351,121 @@ __device__ __forceinline__ void reduce_equations(Eqs& A) {
     const double pv = A.e1[r][3 + r];
     for (int i = r + 1; i <= 5; ++i) row_axpy(A, r, i, 3 + r, A.e1[i][3 + r] / pv);
   }
-  // raise the degree to eliminate the x terms
+  raise_degree(A);
+}
+
+// ---------------------------------------------------------------------------
+// Cooperative reduction: one DPP quad (4 lanes) per hypothesis
+// ---------------------------------------------------------------------------
+// With one lane per hypothesis the reduction was 54 % of k_solve_front's
+// cycles (scripts/front_stats.py): dependent LDS round trips and divisions on
+// waves with 16 of 64 lanes active.  Here the quad holds the ten rows'
+// 20-column vector in registers, lane s the columns k = s + 4m (m < 5):
+//   k 0..9 -> e0[.][k], 10..15 -> e1[.][k-10], 16..18 -> e2[.][k-16], 19 -> e3[.][0]
+// (e3's other columns and e4 first change in raise_degree, which runs on the
+// record afterwards).  Column values the pivot search and the factors need are
+// broadcast within the quad by DPP; every lane divides (same operands, same
+// bits) and updates its own columns.  Each element sees reduce_equations'
+// operations in its order, so the record is bit-identical.
+template <int O>
+__device__ __forceinline__ int quad_bcast_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, O | (O << 2) | (O << 4) | (O << 6), 0xf, 0xf, false);
+}
+
+template <int O>
+__device__ __forceinline__ double quad_bcast(double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)quad_bcast_i<O>((int)(unsigned)u);
+  const unsigned hi = (unsigned)quad_bcast_i<O>((int)(unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// column k's value in row i, from the quad lane that holds it
+template <int K>
+__device__ __forceinline__ double quad_col(const double (&R)[10][5], int i) {
+  return quad_bcast<K & 3>(R[i][K >> 2]);
+}
+
+// does this lane's slot m carry a column row_axpy touches at e0 limit LIM?
+__device__ __forceinline__ bool quad_in(int s, int m, int lim) {
+  const int k = s + 4 * m;
+  return k > 9 || k <= lim;
+}
+
+// rows [I0, I1) -= (row[i][K] / row[PROW][K]) * row PROW   (row_axpy, e0 limit LIM)
+template <int PROW, int K, int I0, int I1, int LIM>
+__device__ __forceinline__ void quad_axpy(double (&R)[10][5], int s) {
+  const double pv = quad_col<K>(R, PROW);
+  double pr[5];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const double f = A.e1[i][3 + i] / A.e0[3 + i][3 + i];
-    A.e4[i] = -A.e3[i + 3][0] * f;
+  for (int m = 0; m < 5; ++m) pr[m] = R[PROW][m];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      A.e3[i][j] -= A.e2[i + 3][j] * f;
-      A.e2[i][j] -= A.e1[i + 3][j] * f;
-      A.e1[i][j] -= A.e0[i + 3][j] * f;
-    }
+  for (int i = I0; i < I1; ++i) {
+    const double fac = quad_col<K>(R, i) / pv;
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+      if (quad_in(s, m, LIM)) R[i][m] -= fac * pr[m];
   }
+}
+
+// pivot_rows + the sweep-up of column C (eliminate_up<C>)
+template <int C>
+__device__ __forceinline__ void quad_eliminate_up(double (&R)[10][5], int s) {
+  constexpr int M = C >> 2;
+  double best = fabs(R[C][M]);
+  int r = C;
+#pragma unroll
+  for (int i = 0; i < C; ++i)
+    if (fabs(R[i][M]) > best) { r = i; best = fabs(R[i][M]); }
+  r = quad_bcast_i<C & 3>(r);                  // the search on the lane holding column C
+  if (r != C) {
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+      if (i == r) {
+#pragma unroll
+        for (int m = 0; m < 5; ++m)
+          if (quad_in(s, m, C)) { const double t = R[C][m]; R[C][m] = R[i][m]; R[i][m] = t; }
+      }
+  }
+  quad_axpy<C, C, 0, C, C>(R, s);
+}
+
+__device__ __forceinline__ int quad_field(int i, int k) {   // offset in the record, in doubles
+  return k < 10 ? i * 10 + k : k < 16 ? 100 + i * 6 + (k - 10) : k < 19 ? 160 + i * 3 + (k - 16) : 190 + i * 3;
+}
+
+// reduce_equations up to (not including) raise_degree, on the record `A`
+// shared by the quad (LDS); lane s = lane & 3.  Callers synchronise the
+// record's writers before and its readers after.
+__device__ __forceinline__ void quad_reduce(Eqs& A, int s) {
+  static_assert(sizeof(Eqs) == 223 * sizeof(double), "record layout");
+  double* f = reinterpret_cast<double*>(&A);
+  double R[10][5];
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+#pragma unroll
+    for (int m = 0; m < 5; ++m) R[i][m] = f[quad_field(i, s + 4 * m)];
+  quad_eliminate_up<9>(R, s);
+  quad_eliminate_up<8>(R, s);
+  quad_eliminate_up<7>(R, s);
+  quad_eliminate_up<6>(R, s);
+  quad_eliminate_up<5>(R, s);
+  quad_eliminate_up<4>(R, s);
+  quad_eliminate_up<3>(R, s);
+  // sweep_down on the w^0 block, rows 3 and 4
+  quad_axpy<3, 3, 4, 6, 3>(R, s);
+  quad_axpy<4, 4, 5, 6, 4>(R, s);
+  // sweep_up on the w^1 block: (row 2, col 5) then (row 1, col 4)
+  quad_axpy<2, 15, 0, 2, 5>(R, s);
+  quad_axpy<1, 14, 0, 1, 4>(R, s);
+  // sweep_down on the w^1 block: (0,3), (1,4), (2,5)
+  quad_axpy<0, 13, 1, 6, 3>(R, s);
+  quad_axpy<1, 14, 2, 6, 4>(R, s);
+  quad_axpy<2, 15, 3, 6, 5>(R, s);
+#pragma unroll
+  for (int i = 0; i < 10; ++i)
+#pragma unroll
+    for (int m = 0; m < 5; ++m) f[quad_field(i, s + 4 * m)] = R[i][m];
 }
 
 // degree-w entry accessor for the reduced 3x3 block

@@ -165,34 +165,83 @@ struct FlowSrc {
 __device__ __forceinline__ double& st_at(double* st, size_t stride, int f, size_t hb) { return st[f * stride + hb]; }
 
 constexpr int kFrontLanes = 16;   // upper bound of the solve_lanes key
-template <class Src>
+
+#ifdef SFM_FRONT_STATS
+// experiment builds only: per wave (lane 0 of each block), the s_memtime
+// stamps at the end of each phase of k_solve_front relative to its start:
+// sample+load, basis, equations, reduction, determinant, state stores
+__device__ unsigned long long g_front_cycles[6][1 << 15];
+#define FRONT_STAMP(i)                                                                          \
+  do {                                                                                          \
+    __builtin_amdgcn_s_waitcnt(0);                                                              \
+    if (threadIdx.x == 0)                                                                       \
+      g_front_cycles[i][(size_t)blockIdx.y * gridDim.x + blockIdx.x] = __builtin_amdgcn_s_memtime() - t_front; \
+  } while (0)
+extern "C" int sfm_experiment_front_stats(unsigned long long* cycles, int n) {
+  return hipMemcpyFromSymbol(cycles, HIP_SYMBOL(g_front_cycles), (size_t)6 * n * 8) == hipSuccess ? 0 : 2;
+}
+#else
+#define FRONT_STAMP(i) do { } while (0)
+#endif
+
+// COOP (tuning key solve_coop, default): the reduction runs on DPP quads,
+// four lanes per hypothesis (quad_reduce in five_point.h), so all 64 lanes of
+// the wave work on the 16 hypotheses' reductions instead of 16 of them.
+template <class Src, bool COOP>
 __global__ __launch_bounds__(64) void k_solve_front(const Src src, PairParams pp, int H, uint64_t seed, int lanes,
                                                     double* __restrict__ st, size_t stride) {
+#ifdef SFM_FRONT_STATS
+  const unsigned long long t_front = __builtin_amdgcn_s_memtime();
+#endif
   const int b = blockIdx.y;
-  if ((int)threadIdx.x >= lanes) return;
-  const int h = blockIdx.x * lanes + threadIdx.x;
-  if (h >= H) return;
-  const int64_t n = pp.n[b];
-  int64_t idx[5];
-  sample5(seed, (uint32_t)h, n, idx);
-  double q[5][2], qp[5][2];
-#pragma unroll
-  for (int d = 0; d < 5; ++d) {
-    const double4 v = src.load(b, idx[d]);
-    q[d][0] = v.x; q[d][1] = v.y; qp[d][0] = v.z; qp[d][1] = v.w;
-  }
-  Lin Eb[9];
-  essential_basis(q, qp, Eb);
-  // The equation set (1784 B) lives in LDS, one record per lane: the
+  // COOP: quad g = lane / 4 carries hypothesis g; its four lanes draw the same
+  // sample and build the same basis (the wave issues those instructions once
+  // either way), then share the equations and the reduction
+  const int g = COOP ? (int)threadIdx.x >> 2 : (int)threadIdx.x;
+  const int qs = (int)threadIdx.x & 3;
+  const int h = blockIdx.x * lanes + g;
+  const bool act = g < lanes && h < H;
+  if (!COOP && !act) return;
+  // The equation set (1784 B) lives in LDS, one record per hypothesis: the
   // reduction's pivoting indexes rows dynamically, which put it in scratch
   // (0.30 -> 0.13 ms per 32,768 hypotheses).  A 1784-B lane stride is 446
   // dwords, so the 16 lanes' doubles fall in distinct bank pairs.
   __shared__ Eqs s_eqs[kFrontLanes];
-  Eqs& A = s_eqs[threadIdx.x];
-  build_equations(Eb, A);
-  reduce_equations(A);
+  Eqs& A = s_eqs[g];
+  double q[5][2], qp[5][2];
+  Lin Eb[9];
+  if (act) {
+    const int64_t n = pp.n[b];
+    int64_t idx[5];
+    sample5(seed, (uint32_t)h, n, idx);
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+      const double4 v = src.load(b, idx[d]);
+      q[d][0] = v.x; q[d][1] = v.y; qp[d][0] = v.z; qp[d][1] = v.w;
+    }
+    FRONT_STAMP(0);
+    essential_basis(q, qp, Eb);
+    FRONT_STAMP(1);
+    if (COOP) {
+      build_equations_quad(Eb, A, qs);
+    } else {
+      build_equations(Eb, A);
+      FRONT_STAMP(2);
+      reduce_equations(A);
+    }
+  }
+  if (COOP) {
+    __syncthreads();                           // the 16 records are written
+    FRONT_STAMP(2);
+    quad_reduce(A, qs);                        // quads of inactive hypotheses reduce unused records
+    __syncthreads();
+    if (!act || qs != 0) return;
+    raise_degree(A);
+  }
+  FRONT_STAMP(3);
   double poly[11];
   determinant_poly(A, poly);
+  FRONT_STAMP(4);
   const size_t hb = (size_t)b * H + h;
 #pragma unroll
   for (int e = 0; e < 9; ++e)
@@ -218,6 +267,7 @@ __global__ __launch_bounds__(64) void k_solve_front(const Src src, PairParams pp
   }
 #pragma unroll
   for (int i = 0; i <= 10; ++i) st_at(st, stride, kStPoly + i, hb) = poly[i];
+  FRONT_STAMP(5);
 }
 
 #ifdef SFM_ROOTS_STATS
@@ -1750,8 +1800,12 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     const int lanes = std::min(tuning().solve_lanes, kFrontLanes);
     const int rlanes = std::min(tuning().roots_lanes, kStkLanes);
     const size_t stride = (size_t)bc * H;
-    hipLaunchKernelGGL(k_solve_front<Src>, dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H, seed,
-                       lanes, w.sstate, stride);
+    if (tuning().solve_coop)
+      hipLaunchKernelGGL((k_solve_front<Src, true>), dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H,
+                         seed, lanes, w.sstate, stride);
+    else
+      hipLaunchKernelGGL((k_solve_front<Src, false>), dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H,
+                         seed, lanes, w.sstate, stride);
     if (tuning().roots_split)
       hipLaunchKernelGGL(k_roots_split, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate,
                          stride, w.nroots);

@@ -92,6 +92,7 @@ _SIGS = [
     ("sfm_tune_set", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("sfm_tune_get", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     ("sfm_profile_enable", ctypes.c_int, [ctypes.c_int]),
+    ("sfm_profile_select", ctypes.c_int, [ctypes.c_char_p]),
     ("sfm_profile_reset", ctypes.c_int, []),
     ("sfm_profile_read", ctypes.c_int,
      [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
@@ -153,6 +154,12 @@ def i64_array(values):
 
 def profile_enable(on=True):
     check(load().sfm_profile_enable(1 if on else 0), "sfm_profile_enable")
+
+
+def profile_select(names=None):
+    """Record only the named kernels (None / empty: all) while profiling is on."""
+    arg = None if not names else ",".join(names).encode()
+    check(load().sfm_profile_select(arg), "sfm_profile_select")
 
 
 def profile_reset():

@@ -394,6 +394,12 @@ int sfm_tune_get(const char* key, int* value);
  * launching stream while enabled).
  * ------------------------------------------------------------------------ */
 int sfm_profile_enable(int on);
+/* Restrict the recording to the comma-separated kernel names in `names`
+ * (NULL or "" = every profiled kernel).  Each recorded launch adds two event
+ * records to its stream (~3.5 us per step per kernel on MI355X between
+ * dependent launches), so bench.py records only the roofline kernels inside
+ * its timed region. */
+int sfm_profile_select(const char* names);
 int sfm_profile_reset(void);
 /* Synchronises the recorded events; total milliseconds and launch count of
  * kernel `name` ("ransac_solve", "ransac_chain", "ransac_score",

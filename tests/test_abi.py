@@ -168,3 +168,16 @@ def test_tuning_keys_round_trip():
         _lib.tune("sweep_nj", old)
     with pytest.raises(Exception):
         _lib.tune_get("no_such_knob")
+
+
+def test_profile_select_filters_names():
+    """sfm_profile_select parses its comma list (CPU: no launches, so every
+    named slot reads zero) and NULL restores recording of every kernel."""
+    from sfm_amd import _lib
+    _lib.profile_select(["ransac_score", "plane_sweep"])
+    _lib.profile_enable(True)
+    _lib.profile_enable(False)
+    assert _lib.profile_read("ransac_score") == (0.0, 0)
+    _lib.profile_select(None)
+    assert _lib.load().sfm_profile_select(b",,ransac_score,") == 0
+    _lib.profile_select(None)
