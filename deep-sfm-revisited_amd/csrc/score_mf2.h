@@ -157,10 +157,26 @@ __device__ __forceinline__ mf_float16 mf2_a(const MfAB& B, mf_half8 A1, mf_half8
 struct MfZ {
   mf_float16 z1, z2;
 };
+#ifndef SFM_MF2_PK
+#define SFM_MF2_PK 0   // measured slower (profiles/r03_mf2_pk_ab.txt)
+#endif
+typedef float mf_float2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ MfZ mf2_z(mf_half8 bd, mf_half8 NL, mf_half8 NH, const mf_float16& a) {
   mf_float16 aa;
+#if SFM_MF2_PK
+  // aa = a * a as eight packed multiplies (v_pk_mul_f32: two IEEE float32
+  // products per instruction, the same bits as v_mul_f32)
+#pragma unroll
+  for (int g = 0; g < 16; g += 2) {
+    mf_float2 v = {a[g], a[g + 1]};
+    v = v * v;
+    aa[g] = v.x;
+    aa[g + 1] = v.y;
+  }
+#else
 #pragma unroll
   for (int g = 0; g < 16; ++g) aa[g] = a[g] * a[g];
+#endif
   MfZ r;
   r.z1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(NL, bd, aa, 0, 0, 0);
   r.z2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(NH, bd, aa, 0, 0, 0);

@@ -32,6 +32,9 @@ if [ "${SKIP_PMC:-0}" != "1" ]; then
       python3 bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-regularize \
       > gpurun_out/r3_prof_c3.log 2>&1 || { tail -20 gpurun_out/r3_prof_c3.log; exit 1; }
 fi
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r3_prof_sparse -o run --output-format csv -- \
+    python3 bench.py --config sparse --steps 10 --warmup 2 --no-cpu-baseline --no-regularize \
+    > gpurun_out/r3_prof_sparse.log 2>&1 || { tail -20 gpurun_out/r3_prof_sparse.log; exit 1; }
 for cfg in sparse c3 c4; do
   timeout -k 10 300 python -u bench.py --config $cfg --steps 20 --warmup 3 --no-cpu-baseline --no-regularize \
       > gpurun_out/r3_bench_$cfg.log 2>&1 || { tail -20 gpurun_out/r3_bench_$cfg.log; exit 1; }
