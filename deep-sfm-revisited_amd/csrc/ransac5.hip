@@ -324,70 +324,119 @@ __global__ __launch_bounds__(64) void k_roots(int H, int lanes, double* __restri
 #endif
 }
 
+// SOLVE_COOP (tuning key solve_coop, default): one DPP quad per hypothesis,
+// lane s taking roots s, s + 4, s + 8; the accepted roots' slots come from a
+// quad-wide mask of the cheirality results, so the writes are the one-lane
+// loop's (accepted E / P in root order; slot 0 = root 0's E when no root is
+// accepted).  Four times the waves of the one-lane kernel, whose 512 waves
+// left half the SIMDs idle and followed each wave's most-rooted hypothesis.
+template <bool COOP>
 __global__ __launch_bounds__(64) void k_solve_back(int H, int cheir, const double* __restrict__ st, size_t stride,
                                                    const int32_t* __restrict__ nroots,
                                                    int32_t* __restrict__ out_ncand, double* __restrict__ hypE,
                                                    double* __restrict__ hypP) {
   const int b = blockIdx.y;
-  const int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= H) return;
-  const size_t hb = (size_t)b * H + h;
-  const int nr = nroots[hb];
+  const int qs = COOP ? (int)threadIdx.x & 3 : 0;
+  const int h = COOP ? blockIdx.x * 16 + ((int)threadIdx.x >> 2) : blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = h < H;
+  if (!COOP && !act) return;
+  const size_t hb = (size_t)b * H + (act ? h : 0);
+  const int nr = act ? nroots[hb] : 0;
   const int nv = nr > 0 ? (nr < 10 ? nr : 10) : 0;
   Lin Eb[9];
-#pragma unroll
-  for (int e = 0; e < 9; ++e)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) Eb[e].c[k] = st[(kStEb + e * 4 + k) * stride + hb];
   Eqs A;   // only the blocks compute_E_matrix reads
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      A.e0[i][j] = st[(kStA + i * 3 + j) * stride + hb];
-      A.e1[i][j] = st[(kStA + 9 + i * 3 + j) * stride + hb];
-      A.e2[i][j] = st[(kStA + 18 + i * 3 + j) * stride + hb];
-      A.e3[i][j] = st[(kStA + 27 + i * 3 + j) * stride + hb];
-    }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) A.e4[i] = st[(kStA + 36 + i) * stride + hb];
   double q[5][2], qp[5][2];
+  if (act) {
 #pragma unroll
-  for (int d = 0; d < 5; ++d) {
-    q[d][0] = st[(kStQ + 4 * d + 0) * stride + hb];
-    q[d][1] = st[(kStQ + 4 * d + 1) * stride + hb];
-    qp[d][0] = st[(kStQ + 4 * d + 2) * stride + hb];
-    qp[d][1] = st[(kStQ + 4 * d + 3) * stride + hb];
+    for (int e = 0; e < 9; ++e)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Eb[e].c[k] = st[(kStEb + e * 4 + k) * stride + hb];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        A.e0[i][j] = st[(kStA + i * 3 + j) * stride + hb];
+        A.e1[i][j] = st[(kStA + 9 + i * 3 + j) * stride + hb];
+        A.e2[i][j] = st[(kStA + 18 + i * 3 + j) * stride + hb];
+        A.e3[i][j] = st[(kStA + 27 + i * 3 + j) * stride + hb];
+      }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) A.e4[i] = st[(kStA + 36 + i) * stride + hb];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+      q[d][0] = st[(kStQ + 4 * d + 0) * stride + hb];
+      q[d][1] = st[(kStQ + 4 * d + 1) * stride + hb];
+      qp[d][0] = st[(kStQ + 4 * d + 2) * stride + hb];
+      qp[d][1] = st[(kStQ + 4 * d + 3) * stride + hb];
+    }
   }
   double* Eo = hypE + hb * kMaxSlots * 9;
   double* Po = hypP + hb * kMaxSlots * 12;
-  int nc = 0;
-  for (int m = 0; m < nv; ++m) {
-    const double w = st[(kStRoots + m) * stride + hb];
-    double E[9];
-    essential_at_root(Eb, A, w, E);
-    if (!cheir) {
+  if (!COOP) {
+    int nc = 0;
+    for (int m = 0; m < nv; ++m) {
+      const double w = st[(kStRoots + m) * stride + hb];
+      double E[9];
+      essential_at_root(Eb, A, w, E);
+      if (!cheir) {
 #pragma unroll
-      for (int e = 0; e < 9; ++e) Eo[m * 9 + e] = E[e];
-      ++nc;
-      continue;
+        for (int e = 0; e < 9; ++e) Eo[m * 9 + e] = E[e];
+        ++nc;
+        continue;
+      }
+      double Pm[12];
+      const bool ok = cheirality_P(E, q, qp, Pm);
+      // compaction (cheirality.cu:142-146): accepted E's move to the front; if
+      // none is accepted slot 0 keeps root 0's E.
+      if (ok) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Eo[nc * 9 + e] = E[e];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) Po[nc * 12 + e] = Pm[e];
+        ++nc;
+      } else if (m == 0) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Eo[e] = E[e];
+      }
     }
-    double Pm[12];
-    const bool ok = cheirality_P(E, q, qp, Pm);
-    // compaction (cheirality.cu:142-146): accepted E's move to the front; if
-    // none is accepted slot 0 keeps root 0's E.
-    if (ok) {
+    out_ncand[hb] = nc;
+    return;
+  }
+  // quad: roots m = qs + 4t
+  double E[3][9], Pm[3][12];
+  int okbits = 0;
 #pragma unroll
-      for (int e = 0; e < 9; ++e) Eo[nc * 9 + e] = E[e];
-#pragma unroll
-      for (int e = 0; e < 12; ++e) Po[nc * 12 + e] = Pm[e];
-      ++nc;
-    } else if (m == 0) {
-#pragma unroll
-      for (int e = 0; e < 9; ++e) Eo[e] = E[e];
+  for (int t = 0; t < 3; ++t) {
+    const int m = qs + 4 * t;
+    if (m < nv) {
+      const double w = st[(kStRoots + m) * stride + hb];
+      essential_at_root(Eb, A, w, E[t]);
+      const bool ok = !cheir || cheirality_P(E[t], q, qp, Pm[t]);
+      if (ok) okbits |= 1 << m;
     }
   }
-  out_ncand[hb] = nc;
+  // the quad's accepted-root mask (roots 0..9), OR-reduced over the four lanes
+  okbits |= __builtin_amdgcn_update_dpp(0, okbits, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  okbits |= __builtin_amdgcn_update_dpp(0, okbits, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  if (!act) return;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int m = qs + 4 * t;
+    if (m < nv) {
+      if ((okbits >> m) & 1) {
+        const int slot = __popc(okbits & ((1 << m) - 1));
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Eo[slot * 9 + e] = E[t][e];
+        if (cheir)
+#pragma unroll
+          for (int e = 0; e < 12; ++e) Po[slot * 12 + e] = Pm[t][e];
+      } else if (m == 0 && okbits == 0) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Eo[e] = E[t][e];
+      }
+    }
+  }
+  if (qs == 0) out_ncand[hb] = __popc(okbits);
 }
 
 // ---------------------------------------------------------------------------
@@ -1812,8 +1861,12 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     else
       hipLaunchKernelGGL(k_roots, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate, stride,
                          w.nroots);
-    hipLaunchKernelGGL(k_solve_back, dim3((H + 63) / 64, bc), dim3(64), 0, s, H, cheir, w.sstate, stride, w.nroots,
-                       w.ncand, w.hypE, w.hypP);
+    if (tuning().solve_coop)
+      hipLaunchKernelGGL(k_solve_back<true>, dim3((H + 15) / 16, bc), dim3(64), 0, s, H, cheir, w.sstate, stride,
+                         w.nroots, w.ncand, w.hypE, w.hypP);
+    else
+      hipLaunchKernelGGL(k_solve_back<false>, dim3((H + 63) / 64, bc), dim3(64), 0, s, H, cheir, w.sstate, stride,
+                         w.nroots, w.ncand, w.hypE, w.hypP);
   }
   SFM_LAUNCHED();
   const int prec = tuning().score_precision;

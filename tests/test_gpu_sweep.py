@@ -9,7 +9,8 @@ coordinates in a different order (and with FMA), which moves them by fp32
 ulps (~1e-5 px at 311 px), and a bilinear sample moves by |grad f| x 1e-5 --
 an error on the scale of the features, independent of how close this one
 value happens to be to zero.  Observed max 3.8e-5 against the reference
-golden, 7.2e-7 against the oracle."""
+golden, 7.2e-7 against the oracle; against the oracle the full-size and
+edge-shape tests also hold the plain relative bar (_close_rel)."""
 import numpy as np
 import pytest
 import torch
@@ -25,6 +26,20 @@ FLOOR = 1.0      # RMS of the N(0,1) features every test samples
 def _close(a, b, floor=FLOOR):
     a = a.float().cpu(); b = b.float().cpu()
     err = (a - b).abs() - RTOL * torch.clamp(b.abs(), min=floor)
+    return float(err.max()) <= 0.0, float((a - b).abs().max())
+
+
+# Against the oracle (the reference's fp32 op order restated, the sample
+# coordinates bit-identical) the bar is north_star's 1e-4 relative itself,
+# with an absolute term 2e-6 (2e-6 of the features' RMS) only for values
+# within ~0.02 of zero, where the 4-tap FMA sum's last-bit differences
+# (<= 7.2e-7 observed) exceed 1e-4 of the value.
+ORACLE_ATOL = 2e-6
+
+
+def _close_rel(a, b):
+    a = a.float().cpu(); b = b.float().cpu()
+    err = (a - b).abs() - (RTOL * b.abs() + ORACLE_ATOL)
     return float(err.max()) <= 0.0, float((a - b).abs().max())
 
 
@@ -73,6 +88,8 @@ def test_full_size_kitti_sweep(cuda):
     got = cost[:, :, planes].cpu()
     assert torch.equal(got[:, :C], want[:, :C])
     ok, err = _close(got[:, C:], want[:, C:])
+    assert ok, err
+    ok, err = _close_rel(got[:, C:], want[:, C:])
     assert ok, err
     # every plane's reference half is the same copy
     assert torch.equal(cost[:, :C, 77].cpu(), ref)
@@ -131,6 +148,8 @@ def test_sweep_shapes_and_depth_modes(cuda, B, C, L, h, w, by_depth):
     want = S.plane_sweep_cost(ref, tgt, pose, K, Ki, L, 0.7, predict_by_depth=by_depth)
     assert torch.equal(got[:, :C].cpu(), want[:, :C])
     ok, err = _close(got[:, C:], want[:, C:])
+    assert ok, err
+    ok, err = _close_rel(got[:, C:], want[:, C:])
     assert ok, err
     assert float(want[:, C:].abs().sum()) > 0.0      # the poses project into the image
 
