@@ -340,6 +340,9 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *
  *   launch shape only -- outputs are bit-identical for every value:
  *     "solve_lanes"           1..16   lanes per wave in k_solve_front (16)
+ *     "solve_coop"            0, 1    k_solve_front's equations and reduction and
+ *                                     k_solve_back on DPP quads, 4 lanes per
+ *                                     hypothesis (1); 0: one lane each
  *     "roots_lanes"           1..32   lanes per wave in k_roots (32)
  *     "sweep_lane_pixels"     0..2    pixel-to-lane mapping of the per-row sweep (0)
  *     "sweep_items_per_block" 1,2,4,8 work items per block of the per-row sweep (4)
