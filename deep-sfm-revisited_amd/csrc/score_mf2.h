@@ -53,6 +53,11 @@
 #ifndef SFM_MF2_BPRE
 #define SFM_MF2_BPRE 0
 #endif
+// queue build: each word's first undecided bit written straight-line, the
+// rare further bits of the same word in a loop behind a wave-uniform test
+#ifndef SFM_MF2_QB
+#define SFM_MF2_QB 0   // 1 measured slower (profiles/r03_mf2_qb_ab.txt)
+#endif
 constexpr int kMf2Waves = SFM_MF2_WAVES;       // 12: 3 per SIMD, two accumulator sets; 16: 4 per SIMD, one
 constexpr int kMf2Wpe = kMf2Waves / 4;
 constexpr int kMf2Span = SFM_MF2_SPAN;         // points per staged span
@@ -511,6 +516,32 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         int pos = incl - nl - base;
         if (qtotal <= kMf2Queue) {
           uint32_t* q = queue + pos;
+#if SFM_MF2_QB
+          uint32_t more = 0u;                                 // words with a second bit (rare)
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const uint32_t uu = mf2_undecided(s1[g], s2[g]);
+            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+            if (uu) {
+              *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
+              more |= (uu & (uu - 1u)) ? (1u << g) : 0u;
+            }
+          }
+          if (__builtin_expect(__builtin_amdgcn_ballot_w64(more != 0u) != 0, 0)) {
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+              if (more & (1u << g)) {
+                uint32_t uu = mf2_undecided(s1[g], s2[g]);
+                uu &= uu - 1u;
+                const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+                while (uu) {
+                  *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
+                  uu &= uu - 1u;
+                }
+              }
+            }
+          }
+#else
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
             uint32_t uu = mf2_undecided(s1[g], s2[g]);
@@ -520,6 +551,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
               uu &= uu - 1u;
             }
           }
+#endif
         } else {
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
