@@ -32,6 +32,7 @@ namespace sfm {
 
 constexpr int kChains = SFM_RANSAC_CHAINS;
 constexpr int kMaxSlots = 10;
+constexpr size_t kMf2ClaimBytes = 8 * sizeof(unsigned long long);   // k_score_mf2's per-XCD claim counters
 constexpr int kCandStride = 18;   // per candidate: E f64[9], Kg, then float[14] (E f32[9], A1, B1, A2, B2, ok32)
 // solve state fields: E basis (36), the 3x3 blocks of the reduced equations
 // that compute_E_matrix reads (39), the five samples (20), det poly (11), roots (10)
@@ -69,7 +70,8 @@ struct Workspace {
   unsigned long long* cov;      // [B][Cmax] pruning bound state: count | points covered << 32
   int32_t* best_lb;             // [64] largest partial count seen (a lower bound on the winning score)
   unsigned long long* skipped;  // [1] evaluations skipped by pruning (whole call)
-  double* pack;        // [n_max][4]
+  unsigned long long* claim;    // [8] k_score_mf2's range-claim counters (zeroed by k_mf_cands)
+  double* pack;        // [n_max][4] (last: its size is the only n_max-dependent one)
 };
 
 __host__ __device__ inline size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
@@ -97,6 +99,9 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   t.skipped = (unsigned long long*)take(8);
   t.score = (int32_t*)take(bc * H * 4);
   t.candF = (_Float16*)take(bc * C * 64 * 2);
+  // before pack: run_packed re-lays the workspace out with n_max = 0, so every
+  // field it uses must sit at an offset independent of n_max
+  t.claim = (unsigned long long*)take(kMf2ClaimBytes);
   t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
   if (w) *w = t;
   return off;
@@ -1710,6 +1715,7 @@ struct ScoreBufs {
   _Float16* candF;
   int32_t* cntT;
   int32_t* cntR;
+  unsigned long long* claim;   // [8] k_score_mf2's range-claim counters
 };
 
 template <class Src>
@@ -1718,11 +1724,11 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
                            bool fast32, int cus, int grid, hipStream_t s) {
   if (use_mf) {
     hipLaunchKernelGGL(k_mf_cands, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax, w.cand_total, w.candE,
-                       w.candF, mp);
+                       w.candF, mp, w.claim);
     const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
     if (same && tuning().score_mf == 2)
       hipLaunchKernelGGL(k_score_mf2<Src>, dim3(std::max(1, cus)), dim3(kMf2Waves * 64), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
+                         w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc, w.claim);
     else if (same)
       hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
@@ -1909,7 +1915,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   }
   {
     ProfScope ps("ransac_score", s);
-    score_dispatch(src, pp, bc, cmax, ScoreBufs{w.cand_total, w.candE, w.candF, w.cntT, w.cntR}, kc, mp, use_mf,
+    score_dispatch(src, pp, bc, cmax, ScoreBufs{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim}, kc, mp, use_mf,
                    same, prec, fast, fast32, cus, grid, s);
   }
   SFM_LAUNCHED();
@@ -2034,7 +2040,8 @@ int sfm_ransac5_flow(const float* flow, int batch, int H, int W, int h_side, int
 size_t sfm_score_essentials_workspace_bytes(int batch, int ncand) {
   if (batch < 1 || batch > SFM_MAX_BATCH || ncand < 1) return 0;
   const size_t c = (size_t)batch * ncand;
-  return align_up(SFM_MAX_BATCH * 4) + align_up(c * kCandStride * 8) + align_up(c * kMfRec * 2) + align_up(c * 4);
+  return align_up(SFM_MAX_BATCH * 4) + align_up(c * kCandStride * 8) + align_up(c * kMfRec * 2) + align_up(c * 4) +
+         align_up(kMf2ClaimBytes);
 }
 
 int sfm_score_essentials(const double* pts, int64_t n_stride, const int64_t* n, int batch, const double* E,
@@ -2062,6 +2069,8 @@ int sfm_score_essentials(const double* pts, int64_t n_stride, const int64_t* n, 
   w.candF = (_Float16*)p;
   p += align_up(c * kMfRec * 2);
   w.cntR = (int32_t*)p;
+  p += align_up(c * 4);
+  w.claim = (unsigned long long*)p;
   w.cntT = counts;
   PairParams pp{};
   for (int b = 0; b < batch; ++b) {

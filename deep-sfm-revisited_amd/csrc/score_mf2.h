@@ -55,6 +55,17 @@
 #endif
 // queue build: each word's first undecided bit written straight-line, the
 // rare further bits of the same word in a loop behind a wave-uniform test
+#ifndef SFM_MF2_DYN
+#define SFM_MF2_DYN 1
+#endif
+#ifndef SFM_MF2_MINCHUNK
+#define SFM_MF2_MINCHUNK 128
+#endif
+constexpr int kMf2MinChunk = SFM_MF2_MINCHUNK;               // smallest claimed unit range (candidate tiles)
+#ifndef SFM_MF2_GUIDE
+#define SFM_MF2_GUIDE 2
+#endif
+constexpr int kMf2Guide = SFM_MF2_GUIDE;                     // a claim takes remainder / (guide x blocks per XCD)
 #ifndef SFM_MF2_QB
 #define SFM_MF2_QB 0   // 1 measured slower (profiles/r03_mf2_qb_ab.txt)
 #endif
@@ -208,11 +219,17 @@ __device__ __forceinline__ int mf2_lane() {
   return l;
 }
 
+#ifdef SFM_MF2_BLOCKT
+__device__ unsigned long long g_mf2_blockt[3 * 4096];
+extern "C" int sfm_experiment_mf2_blockt(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mf2_blockt), (size_t)3 * n * 8) == hipSuccess ? 0 : 2;
+}
+#endif
 template <class Src>
 __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(kMf2Wpe, kMf2Wpe))) void k_score_mf2(
     const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
     const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
-    int32_t* __restrict__ cntR, ScoreConsts kc) {
+    int32_t* __restrict__ cntR, ScoreConsts kc, unsigned long long* __restrict__ claim) {
   __shared__ __attribute__((aligned(16))) _Float16 s_frag[kMf2Tiles][3][64][8];
   __shared__ double4 s_pts[kMf2Span];
   __shared__ uint32_t s_queue[kMf2Waves][kMf2Queue];
@@ -221,6 +238,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   __shared__ int32_t s_tiles[SFM_MAX_BATCH];                 // candidate tiles per pair
   __shared__ int32_t s_ctot[SFM_MAX_BATCH];
   __shared__ int32_t s_claim;                                // next candidate tile of the span to claim
+  __shared__ long long s_range[2];                           // the block's current unit range
   const int tid = threadIdx.x, wv = tid >> 6;
   if (tid == 0) {
     long long acc = 0;
@@ -237,13 +255,30 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   }
   for (int i = tid; i < kMf2Waves * kKC; i += kMf2Waves * 64) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
-  // XCD-aware contiguous ranges: workgroup ids are dealt round-robin over the
-  // 8 XCDs, so id % 8 names the XCD; logical block = XCD-major.
+#ifdef SFM_MF2_BLOCKT
+  const unsigned long long blk_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // Unit ranges: workgroup ids are dealt round-robin over the 8 XCDs, so
+  // id % 8 names the XCD.  SFM_MF2_DYN (default): XCD x owns the x-th eighth
+  // of the units (about one pair, whose A rows then stay in that XCD's L2),
+  // and its blocks claim guided chunks of it from a global counter (half the
+  // remainder's per-block share, at least kMf2MinChunk units); a block whose
+  // eighth is exhausted takes chunks of the next XCDs' eighths.  Static
+  // contiguous ranges left blocks idle for 6 % of the launch on average
+  // (scripts/mf2_blockt.py): units cost unequal time across pairs and XCDs.
   const int G = gridDim.x;
+  const long long U = s_first[batch];
+#if SFM_MF2_DYN
+  const int nx = (G % 8 == 0) ? 8 : 1;
+  const int xcd = (int)(blockIdx.x % (unsigned)nx);
+  const int per_x = G / nx;
+  int victim = 0;                                            // XCDs after our own already drained
+  long long units_done = 0;
+#else
   const int per_xcd = G / 8;
   const int logical = (G % 8 == 0) ? (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  const long long U = s_first[batch];
   const long long u_beg = U * logical / G, u_end = U * (logical + 1) / G;
+#endif
 #if !SFM_MF2_CARRY
   int32_t* cnt = s_cnt[wv];
 #endif
@@ -251,7 +286,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   const _Float16* fr = &s_frag[0][0][0][0];
   constexpr int kTileHalves = 3 * 64 * 8;
   int b = 0;
+#if !SFM_MF2_DYN
   long long u = u_beg;
+#endif
   mf_half8 A1, A2, AL, AH;
 #ifdef SFM_MF_STAMPS
   // experiment builds (scripts/mf_stamps.py): [0] staging, [1] tile loop,
@@ -284,6 +321,34 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       }
     }
   };
+#if SFM_MF2_DYN
+  for (;;) {
+    if (tid == 0) {
+      long long st = U, en = U;
+      for (; victim < nx; ++victim) {
+        const int x = (xcd + victim) % nx;
+        const long long seg_beg = U * x / nx, seg_end = U * (x + 1) / nx;
+        const long long rem = seg_end - seg_beg - (long long)__hip_atomic_load(claim + x, __ATOMIC_RELAXED,
+                                                                                __HIP_MEMORY_SCOPE_AGENT);
+        if (rem <= 0) continue;
+        const long long size = max((long long)kMf2MinChunk, rem / (kMf2Guide * per_x));
+        const long long got = seg_beg + (long long)atomicAdd(claim + x, (unsigned long long)size);
+        if (got < seg_end) {
+          st = got;
+          en = min(got + size, seg_end);
+          break;
+        }
+      }
+      s_range[0] = st;
+      s_range[1] = en;
+    }
+    __syncthreads();
+    long long u = s_range[0];
+    const long long u_end = s_range[1];
+    if (u >= u_end) break;
+    units_done += u_end - u;
+    if (u < s_first[b]) b = 0;                               // a stolen chunk may lie before our own
+#endif
   while (u < u_end) {
     while (u >= s_first[b + 1]) ++b;
     b = __builtin_amdgcn_readfirstlane(b);
@@ -604,8 +669,25 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     lds_barrier();                                            // the span is re-staged next
     MF_STAMP(5);
   }
+#if SFM_MF2_DYN
+  }
+#endif
 #ifdef SFM_MF_STAMPS
   if (mf2_lane() == 0)
     for (int i = 0; i < kMfStamps; ++i) atomicAdd(&g_mf_stamps[i], mf_acc_[i]);
+#endif
+#ifdef SFM_MF2_BLOCKT
+  // experiment builds (scripts/mf2_blockt.py): each block's start and end on
+  // the 100 MHz clock and its unit count, for the cross-block balance
+  __syncthreads();
+  if (tid == 0) {
+    g_mf2_blockt[blockIdx.x * 3 + 0] = blk_t0;
+    g_mf2_blockt[blockIdx.x * 3 + 1] = __builtin_amdgcn_s_memrealtime();
+#if SFM_MF2_DYN
+    g_mf2_blockt[blockIdx.x * 3 + 2] = (unsigned long long)units_done;
+#else
+    g_mf2_blockt[blockIdx.x * 3 + 2] = (unsigned long long)(u_end - u_beg);
+#endif
+  }
 #endif
 }
