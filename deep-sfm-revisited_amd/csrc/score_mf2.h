@@ -331,7 +331,10 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         const long long rem = seg_end - seg_beg - (long long)__hip_atomic_load(claim + x, __ATOMIC_RELAXED,
                                                                                 __HIP_MEMORY_SCOPE_AGENT);
         if (rem <= 0) continue;
-        const long long size = max((long long)kMf2MinChunk, rem / (kMf2Guide * per_x));
+        // the floor never exceeds a block's static share of the eighth (small
+        // launches, e.g. 2,048 keypoints: a 128-unit floor would idle most blocks)
+        const long long floor_c = min((long long)kMf2MinChunk, (seg_end - seg_beg + per_x - 1) / per_x);
+        const long long size = max(max(floor_c, 1ll), rem / (kMf2Guide * per_x));
         const long long got = seg_beg + (long long)atomicAdd(claim + x, (unsigned long long)size);
         if (got < seg_end) {
           st = got;
