@@ -62,6 +62,9 @@
 #define SFM_MF2_MINCHUNK 128
 #endif
 constexpr int kMf2MinChunk = SFM_MF2_MINCHUNK;               // smallest claimed unit range (candidate tiles)
+#ifndef SFM_MF2_ALIGN
+#define SFM_MF2_ALIGN 0   // 1 measured slower (profiles/r03_mf2_align_ab.txt)
+#endif
 #ifndef SFM_MF2_GUIDE
 #define SFM_MF2_GUIDE 2
 #endif
@@ -328,19 +331,47 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       for (; victim < nx; ++victim) {
         const int x = (xcd + victim) % nx;
         const long long seg_beg = U * x / nx, seg_end = U * (x + 1) / nx;
+        // the floor never exceeds a block's static share of the eighth (small
+        // launches, e.g. 2,048 keypoints: a 128-unit floor would idle most blocks)
+        const long long floor_c = max(min((long long)kMf2MinChunk, (seg_end - seg_beg + per_x - 1) / per_x), 1ll);
+#if SFM_MF2_ALIGN
+        // chunks of a span or more end on a span boundary, so that a span is
+        // staged by one block only (compare-and-swap on the claimed offset)
+        unsigned long long cur = __hip_atomic_load(claim + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool done = false;
+        while (seg_beg + (long long)cur < seg_end) {
+          const long long start = seg_beg + (long long)cur, rem = seg_end - start;
+          long long end = min(start + max(floor_c, rem / (kMf2Guide * per_x)), seg_end);
+          int pb = 0;
+          while (end > s_first[pb + 1]) ++pb;                  // the pair holding unit end - 1
+          const long long tl = s_tiles[pb];
+          if (end - start >= tl) {
+            const long long loc = end - s_first[pb];
+            end = min(s_first[pb] + (loc + tl - 1) / tl * tl, seg_end);
+          }
+          const unsigned long long want = (unsigned long long)(end - seg_beg);
+          const unsigned long long seen = atomicCAS(claim + x, cur, want);
+          if (seen == cur) {
+            st = start;
+            en = end;
+            done = true;
+            break;
+          }
+          cur = seen;
+        }
+        if (done) break;
+#else
         const long long rem = seg_end - seg_beg - (long long)__hip_atomic_load(claim + x, __ATOMIC_RELAXED,
                                                                                 __HIP_MEMORY_SCOPE_AGENT);
         if (rem <= 0) continue;
-        // the floor never exceeds a block's static share of the eighth (small
-        // launches, e.g. 2,048 keypoints: a 128-unit floor would idle most blocks)
-        const long long floor_c = min((long long)kMf2MinChunk, (seg_end - seg_beg + per_x - 1) / per_x);
-        const long long size = max(max(floor_c, 1ll), rem / (kMf2Guide * per_x));
+        const long long size = max(floor_c, rem / (kMf2Guide * per_x));
         const long long got = seg_beg + (long long)atomicAdd(claim + x, (unsigned long long)size);
         if (got < seg_end) {
           st = got;
           en = min(got + size, seg_end);
           break;
         }
+#endif
       }
       s_range[0] = st;
       s_range[1] = en;
