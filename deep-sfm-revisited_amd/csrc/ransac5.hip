@@ -32,7 +32,7 @@ namespace sfm {
 
 constexpr int kChains = SFM_RANSAC_CHAINS;
 constexpr int kMaxSlots = 10;
-constexpr size_t kMf2ClaimBytes = 8 * sizeof(unsigned long long);   // k_score_mf2's per-XCD claim counters
+constexpr size_t kMf2ClaimBytes = 9 * sizeof(unsigned long long);   // k_score_mf2's per-XCD claim counters + done
 constexpr int kCandStride = 18;   // per candidate: E f64[9], Kg, then float[14] (E f32[9], A1, B1, A2, B2, ok32)
 // solve state fields: E basis (36), the 3x3 blocks of the reduced equations
 // that compute_E_matrix reads (39), the five samples (20), det poly (11), roots (10)
@@ -70,7 +70,7 @@ struct Workspace {
   unsigned long long* cov;      // [B][Cmax] pruning bound state: count | points covered << 32
   int32_t* best_lb;             // [64] largest partial count seen (a lower bound on the winning score)
   unsigned long long* skipped;  // [1] evaluations skipped by pruning (whole call)
-  unsigned long long* claim;    // [8] k_score_mf2's range-claim counters (zeroed by k_mf_cands)
+  unsigned long long* claim;    // [9] k_score_mf2's range-claim counters and finished-block count (zero between launches)
   double* pack;        // [n_max][4] (last: its size is the only n_max-dependent one)
 };
 
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(64) void k_solve_front(const Src src, PairParams pp
   if (COOP) {
     __syncthreads();                           // the 16 records are written
     FRONT_STAMP(2);
-    quad_reduce(A, qs);                        // quads of inactive hypotheses reduce unused records
+    if (act) quad_reduce(A, qs);               // act is uniform per quad: its DPP exchanges stay within it
     __syncthreads();
     if (!act || qs != 0) return;
     raise_degree(A);
@@ -1715,7 +1715,7 @@ struct ScoreBufs {
   _Float16* candF;
   int32_t* cntT;
   int32_t* cntR;
-  unsigned long long* claim;   // [8] k_score_mf2's range-claim counters
+  unsigned long long* claim;   // [9] k_score_mf2's range-claim counters and finished-block count
 };
 
 template <class Src>

@@ -166,8 +166,9 @@ __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, con
                            _Float16* __restrict__ candF, MfParams mp, unsigned long long* __restrict__ claim) {
   const int b = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  // k_score_mf2's range-claim counters (one per XCD) start every launch at 0
-  if (claim && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 8) claim[threadIdx.x] = 0ull;
+  // k_score_mf2's range-claim counters (one per XCD) and its finished-block
+  // count start every launch at 0
+  if (claim && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 9) claim[threadIdx.x] = 0ull;
   if (c >= cand_total[b]) return;
   const double* E = candE + ((size_t)b * cmax + c) * kCandStride;
   _Float16 row[kMfRec];

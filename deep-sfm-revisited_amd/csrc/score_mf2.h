@@ -706,6 +706,18 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #if SFM_MF2_DYN
   }
 #endif
+#if SFM_MF2_DYN
+  // the last block out zeroes the counters (claim[8] counts finished blocks),
+  // so the workspace holds no schedule-dependent bytes after the launch
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    if (atomicAdd(claim + 8, 1ull) == (unsigned long long)G - 1ull) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) claim[i] = 0ull;
+    }
+  }
+#endif
 #ifdef SFM_MF_STAMPS
   if (mf2_lane() == 0)
     for (int i = 0; i < kMfStamps; ++i) atomicAdd(&g_mf_stamps[i], mf_acc_[i]);

@@ -57,3 +57,19 @@ def test_solve_coop_bit_identical(cuda, mode, lanes, iters):
     assert int(diff.sum()) <= 64
     for a, b in zip(out0, out1):
         assert torch.equal(a, b)
+
+
+def test_pose_workspace_repeatable(cuda):
+    """Two identical pose stages leave byte-identical workspaces: nothing
+    schedule-dependent survives a launch (k_score_mf2's range-claim counters
+    are zeroed by its last block; the float64 drains only add counts)."""
+    from sfm_amd import synth
+    from sfm_amd.pipeline import TwoViewHotPath
+    B = 8
+    flow, K, _, _ = synth.kitti_pair_batch(B, seed=1008, device=cuda)
+    hp = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 128, 8, 1e-4, 1.0, True, 0.6, device=cuda)
+    ws0, out0 = _pose_workspace(hp, flow, K, 1, 16)
+    ws1, out1 = _pose_workspace(hp, flow, K, 1, 16)
+    assert torch.equal(ws0, ws1)
+    for a, b in zip(out0, out1):
+        assert torch.equal(a, b)
