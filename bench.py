@@ -98,6 +98,33 @@ def parse(argv=None):
     return args
 
 
+def src_hash():
+    """Hash of the kernel and C-ABI sources (comments and whitespace removed,
+    so documentation edits keep it): ties a committed rocprofv3 / PMC summary
+    to the code it was recorded from."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "deep-sfm-revisited_amd", "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".h", ".cpp")))
+    for f in [os.path.join(csrc, f) for f in files] + [os.path.join(ROOT, "include", "sfm_hip.h")]:
+        t = open(f).read()
+        t = re.sub(r"/\*.*?\*/", " ", t, flags=re.S)
+        t = re.sub(r"//[^\n]*", " ", t)
+        h.update(os.path.basename(f).encode() + b"\0" + " ".join(t.split()).encode() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def _profile_hash(path):
+    """src_hash a committed summary was recorded with: a PMC summary's own
+    "src_hash" field, or a stats CSV's sidecar <name>.meta.json."""
+    try:
+        if path.endswith(".json"):
+            return json.load(open(path)).get("src_hash")
+        return json.load(open(path[:-4] + ".meta.json")).get("src_hash")
+    except (OSError, ValueError):
+        return None
+
+
 def _round_version(path):
     """profiles/r02_pmc_v10.json -> (2, 10): numeric, so v10 sorts after v6
     (an optional config tag, r02_pmc_c3_v1.json, is allowed)."""
@@ -109,9 +136,12 @@ def pmc_traffic(args):
     """HBM bytes per launch of the path's kernels from the newest committed PMC
     summary (profiles/rNN_pmc[_vK].json, scripts/gpu_pmc.sh + scripts/pmc_summary.py;
     counters need their own profiler pass, so they cannot be read live here).
-    Only reported for the workload the summary was collected on."""
+    Only reported for the workload the summary was collected on, and only from
+    a summary recorded from these sources (src_hash)."""
     import glob
-    fs = [f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json")) if _round_version(f)[0] >= 0]
+    cur = src_hash()
+    fs = [f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json"))
+          if _round_version(f)[0] >= 0 and _profile_hash(f) == cur]
     fs.sort(key=_round_version)
     for f in reversed(fs):
         d = json.load(open(f))
@@ -137,13 +167,15 @@ def rocprof_kernel_ms(args, prefixes):
     summary of this workload (profiles/rNN_kernel_stats[_cfg]_vK.csv, written
     by scripts/gpu_profile.sh from a profiled run of this bench), so the line
     carries a frac that follows from the committed profile, beside the live
-    HIP-event one."""
+    HIP-event one.  Only a summary recorded from these sources counts
+    (its .meta.json sidecar's src_hash)."""
     import csv
     import glob
     best = None
+    cur = src_hash()
     for f in glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats*.csv")):
         v = _stats_version(f)
-        if v and v[0] == args.config and (best is None or v[1] > best[0]):
+        if v and v[0] == args.config and _profile_hash(f) == cur and (best is None or v[1] > best[0]):
             best = (v[1], f)
     if best is None:
         return None, None
@@ -317,6 +349,12 @@ def regularize_roofline(cost, steps=3, precision="bf16"):
             "note": "not part of value: the CNN after the measured path, timed after it"}
 
 
+def rank_device_index(local):
+    """The GPU a rank drives: its LOCAL_RANK (one process per GPU of the node;
+    dist.init binds the RCCL communicator to the same index)."""
+    return int(local)
+
+
 def _stub_mode():
     """SFM_BENCH_CPU_STUB=1: CPU-only rehearsal of the launch / rank / timing
     control flow (gloo, a small torch matmul as the step).  Used by
@@ -346,7 +384,7 @@ def main(argv=None):
 
 def _main_stub(args, dist):
     import torch
-    rank, world, _ = dist.init(backend="gloo")
+    rank, world, _local = dist.init(backend="gloo")
     x = torch.randn(64, 64, generator=torch.Generator().manual_seed(rank))
     for _ in range(args.warmup):
         x = torch.tanh(x @ x)
@@ -357,8 +395,9 @@ def _main_stub(args, dist):
     dist.barrier()
     elapsed = dist.reduce_max(time.perf_counter() - t0)
     names = dist.device_names(None)
-    # the same per-pair gather as the GPU path: rows tagged (rank, pair)
-    rows = torch.tensor([[float(rank), float(i)] for i in range(args.batch)], dtype=torch.float64)
+    # the same per-pair gather as the GPU path: rows tagged (rank, device index, pair)
+    di = rank_device_index(_local)
+    rows = torch.tensor([[float(rank), float(di), float(i)] for i in range(args.batch)], dtype=torch.float64)
     gathered = dist.gather_rows(rows, world)
     if rank == 0:
         print(json.dumps({"metric": "stub", "value": world * args.batch * args.steps / elapsed, "unit": "pairs/s",
@@ -379,7 +418,7 @@ def _main_gpu(args, dist):
     from sfm_amd import _lib, ransac, synth
     from sfm_amd.pipeline import TwoViewHotPath
     rank, world, local = dist.init()
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", rank_device_index(local))
     torch.cuda.set_device(dev)
     B = args.batch
     if args.hw_name == "kitti":
@@ -464,6 +503,7 @@ def _main_gpu(args, dist):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            "src_hash": src_hash(),
             "dtype": "f64+" + ("f32" if s == 4 else "bf16"),
             "data": (f"synthetic (seeded {hwtxt.split()[0]}-shaped rigid scene, 0.5 px noise, 15% outlier flow, "
                      f"{corr}; N(0,1) features)"),

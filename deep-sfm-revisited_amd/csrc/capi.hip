@@ -121,6 +121,7 @@ const TuneKey kTuneKeys[] = {
     {"score_interleave", &sfm::Tuning::score_interleave, v_01},
     {"conv_rolling", &sfm::Tuning::conv_rolling, v_01},
     {"score_precision", &sfm::Tuning::score_precision, [](int v) { return v == 64 || v == 32 || v == 16; }},
+    {"score_lowp_template", &sfm::Tuning::score_lowp_template, v_01},
 };
 const TuneKey* find_key(const char* key) {
   for (const TuneKey& k : kTuneKeys)

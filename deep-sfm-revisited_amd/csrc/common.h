@@ -35,6 +35,8 @@ struct Tuning {
   int score_interleave = 0;      // k_score32 items: pairs interleaved (1) or pair after pair (0)
   int score_precision = 64;      // 64: exact (reference float64 decisions); 32 / 16: ComputeError<float> /
                                  // <half> semantics (approximate inlier sets, BASELINE C5)
+  int score_lowp_template = 0;   // 32 / 16: 0 = E and every operation held in T (this build's variant);
+                                 // 1 = the literal ComputeError<T> with double Ematrix (double products)
   int conv_rolling = 1;          // 1: cin-32 conv layers roll along the planes (k_conv3r); 0: k_conv3
 };
 Tuning& tuning();

@@ -721,21 +721,98 @@ __device__ __forceinline__ bool inlier_test(const double* E, const Addends& ad, 
 }
 
 // Reduced-precision scoring (tuning key score_precision; BASELINE C5's fp32 vs
-// fp16 inlier-set sweep).  ComputeError<T> (kernel_functions.cu:232-264) with
-// the Ematrix, q and qp held in T: every operation of the reference's
-// expression tree rounded to T (RNE, source order, no contraction), sqrt and
-// division correctly rounded in T, and the reference call site's test
-// `error <= c_inlier_threshold` against the float64 threshold
-// (kernel_functions.cu:193-194).  E is first scaled by a power of two (exact;
-// the error is invariant to the scale of E).  Inputs reach T through float32
-// (float64 -> float32 -> T), as the conversion hardware does.  For T = half the sqrt and
-// the division run in float32 and round once to half: float32 carries
-// 24 >= 2*11 + 2 bits, so that double rounding is exact (the result is the
-// correctly rounded half).  oracle/ransac5_oracle.cpp:is_inlier_lp restates it.
+// fp16 inlier-set sweep).  Two forms; the reference itself only ever
+// instantiates ComputeError<double> (kernel_functions.cu:193, 210), so neither
+// has a reference output and both are pinned only to this build's oracle
+// restatement (parity unpinned against the reference):
+//   * "held in T" (score_precision 32 / 16, inlier_lowp below): this build's
+//     own variant, NOT the reference's template.  E, q, qp and every
+//     operation of ComputeError's expression tree in T (RNE, source order, no
+//     contraction), sqrt and division correctly rounded in T.  E is first
+//     scaled by a power of two (exact; the error is invariant to the scale of
+//     E).  Inputs reach T through float32 (float64 -> float32 -> T).  For T =
+//     half the sqrt and the division run in float32 and round once to half:
+//     float32 carries 24 >= 2*11 + 2 bits, so that double rounding is exact.
+//     oracle/ransac5_oracle.cpp:is_inlier_lp restates it.
+//   * "template" (score_lowp_template 1, inlier_lowp_tpl): what a literal
+//     ComputeError<T> instantiation computes with the reference's Ematrix =
+//     double[3][3] (common.h:26).  q, qp are T; each E[k][l] * q[l] is a
+//     double product (T widened exactly), `sum += ...` adds in double and
+//     rounds the sum to T; xEx, D, sqrt and the division are T arithmetic.
+//     No scaling of E.  oracle/ransac5_oracle.cpp:is_inlier_lp_tpl restates it.
+// Both end with the call site's `error <= c_inlier_threshold` against the
+// float64 threshold (kernel_functions.cu:193-194).
 template <int PREC>
 struct LowP { using T = float; };
 template <>
 struct LowP<16> { using T = _Float16; };
+template <>
+struct LowP<17> { using T = _Float16; };
+
+// float64 -> binary16, rounded once (ties to even; subnormals; overflow to
+// inf): the conversion of `T q_test[3] = {qs[..], ...}` for T = half.  The
+// quantum arithmetic is exact in float64 (oracle: h16d).
+__device__ __forceinline__ _Float16 h16_of_double(double v) {
+  if (!(fabs(v) < 65520.0)) return (_Float16)(float)v;       // inf / nan / past max + half an ulp
+  const double a = fabs(v);
+  double q;
+  if (a < 0x1p-14) {
+    q = 0x1p-24;
+  } else {
+    int e;
+    (void)frexp(a, &e);
+    q = ldexp(1.0, e - 1 - 10);
+  }
+  return (_Float16)(float)copysign(rint(a / q) * q, v);      // representable: the conversions are exact
+}
+__device__ __forceinline__ float lowp_of_double(double v, float) { return (float)v; }
+__device__ __forceinline__ _Float16 lowp_of_double(double v, _Float16) { return h16_of_double(v); }
+
+// the literal template form (PREC 33 = float, 17 = half; see above)
+template <int PREC>
+__device__ __forceinline__ bool inlier_lowp_tpl(const double* E, double xd, double yd, double xpd, double ypd,
+                                                double thr) {
+  using T = typename LowP<PREC>::T;
+  const T q[3] = {lowp_of_double(xd, T()), lowp_of_double(yd, T()), (T)1.0f};
+  const T qp[3] = {lowp_of_double(xpd, T()), lowp_of_double(ypd, T()), (T)1.0f};
+  T Ex[3], xE[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    T sum = (T)0.0f;
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+      const double p = E[3 * k + l] * (double)q[l];
+      const double t = (double)sum + p;
+      sum = lowp_of_double(t, T());
+    }
+    Ex[k] = sum;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    T sum = (T)0.0f;
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+      const double p = (double)qp[l] * E[3 * l + k];
+      const double t = (double)sum + p;
+      sum = lowp_of_double(t, T());
+    }
+    xE[k] = sum;
+  }
+  T xEx = (T)0.0f, m;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    m = qp[k] * Ex[k];
+    xEx = xEx + m;
+  }
+  T D, m0, m1;
+  m0 = Ex[0] * Ex[0]; m1 = Ex[1] * Ex[1]; D = m0 + m1;
+  m0 = xE[0] * xE[0]; D = D + m0;
+  m0 = xE[1] * xE[1]; D = D + m0;
+  const T d = (T)sqrtf((float)D);
+  T err = (T)((float)xEx / (float)d);
+  if (err < (T)0.0f) err = -err;
+  return (double)(float)err <= thr;
+}
 
 template <int PREC>
 __device__ __forceinline__ bool inlier_lowp(const double* E, double xd, double yd, double xpd, double ypd,
@@ -798,7 +875,8 @@ __device__ __forceinline__ void score_chunk(const double* __restrict__ CE, int n
 #pragma unroll
     for (int k = 0; k < kPPL; ++k) {
       const bool in = PREC == 64 ? inlier_test<FAST, UNITM>(E, ad, Kg, x[k], y[k], xp[k], yp[k], mm2[k], kc)
-                                 : inlier_lowp<PREC>(E, x[k], y[k], xp[k], yp[k], kc.thr);
+                      : (PREC & 1) ? inlier_lowp_tpl<PREC>(E, x[k], y[k], xp[k], yp[k], kc.thr)
+                                   : inlier_lowp<PREC>(E, x[k], y[k], xp[k], yp[k], kc.thr);
       const uint64_t m = __ballot(in);
       sT += __popcll(m & mT[k]);
       if (!SAME) sR += __popcll(m & mR[k]);
@@ -1718,6 +1796,13 @@ struct ScoreBufs {
   unsigned long long* claim;   // [9] k_score_mf2's range-claim counters and finished-block count
 };
 
+// score_precision with the low-precision form folded in: 64, 32 / 16 (held in
+// T), 33 / 17 (the literal template form, score_lowp_template)
+static int lowp_prec() {
+  const int p = tuning().score_precision;
+  return (p != 64 && tuning().score_lowp_template) ? p + 1 : p;
+}
+
 template <class Src>
 static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cmax, const ScoreBufs& w,
                            const ScoreConsts& kc, const MfParams& mp, bool use_mf, bool same, int prec, bool fast,
@@ -1728,7 +1813,7 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
     const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
     if (same && tuning().score_mf == 2)
       hipLaunchKernelGGL(k_score_mf2<Src>, dim3(std::max(1, cus)), dim3(kMf2Waves * 64), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc, w.claim);
+                         w.cand_total, w.candE, w.candF, w.cntT, kc, w.claim);
     else if (same)
       hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
@@ -1740,6 +1825,12 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
                        w.cand_total, w.candE, w.cntT, w.cntR, kc);
   else if (prec == 16)
     hipLaunchKernelGGL((k_score<false, Src, 16>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
+                       w.cand_total, w.candE, w.cntT, w.cntR, kc);
+  else if (prec == 33)
+    hipLaunchKernelGGL((k_score<false, Src, 33>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
+                       w.cand_total, w.candE, w.cntT, w.cntR, kc);
+  else if (prec == 17)
+    hipLaunchKernelGGL((k_score<false, Src, 17>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                        w.cand_total, w.candE, w.cntT, w.cntR, kc);
   else if (fast32 && same && tuning().score_mfma)
     hipLaunchKernelGGL(k_score_mx<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax, w.cand_total,
@@ -1875,7 +1966,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                          w.nroots, w.ncand, w.hypE, w.hypP);
   }
   SFM_LAUNCHED();
-  const int prec = tuning().score_precision;
+  const int prec = lowp_prec();
   // reduced precision: no exactness guards; the plain ComputeError<T> kernel
   const bool fast = prec == 64 && thr >= 0x1p-40 && thr < 1.0;
   const double guard_g = fast ? 0x1p24 * (11.0 + 11.0 / thr) : 0.0;
@@ -1921,8 +2012,10 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   SFM_LAUNCHED();
   {
     ProfScope ps("ransac_select", s);
+    // k_score_mf2 publishes one count array (its runs have num_test == num_ransac_test)
+    const bool one_cnt = use_mf && same && tuning().score_mf == 2;
     hipLaunchKernelGGL(k_select, dim3(bc), dim3(1024), 0, s, H, cmax, cheir, w.ncand, w.cand_off, w.cntT,
-                       w.cntR, w.candE, w.hypP, w.hypP0, score_out ? score_out : w.score, E_out, P_out,
+                       one_cnt ? w.cntT : w.cntR, w.candE, w.hypP, w.hypP0, score_out ? score_out : w.score, E_out, P_out,
                        inliers_out, winner_out);
   }
   SFM_LAUNCHED();
@@ -2078,7 +2171,7 @@ int sfm_score_essentials(const double* pts, int64_t n_stride, const int64_t* n, 
     pp.test[b] = pp.rtest[b] = (int32_t)n[b];
     pp.splits[b] = (int32_t)((n[b] + kPtsPerItem - 1) / kPtsPerItem);
   }
-  const int prec = tuning().score_precision;
+  const int prec = lowp_prec();
   const bool fast = prec == 64 && thr >= 0x1p-40 && thr < 1.0;
   const double guard_g = fast ? 0x1p24 * (11.0 + 11.0 / thr) : 0.0;
   const bool fast32 = fast && thr >= 0x1p-20 && tuning().score_fp32;

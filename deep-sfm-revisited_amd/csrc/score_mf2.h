@@ -44,8 +44,23 @@
 #ifndef SFM_MF2_WAVES
 #define SFM_MF2_WAVES 12
 #endif
-#ifndef SFM_MF2_CARRY
-#define SFM_MF2_CARRY 0
+// Per-block LDS count table (round 4): a run's counts are added into an LDS
+// table of the pair's candidates (tile k of a span belongs to one wave, and a
+// block barrier separates spans, so the adds need no atomics); the table goes
+// to the global counts with one atomic per nonzero candidate when the block
+// moves to another pair or ends.  Round 3 published every (span, candidate)
+// with two global atomics: 0.27 GB of atomic traffic per launch at C2.
+// SFM_MF2_TBL 2: 16-bit counts, two per LDS word (ds_add_u32 of d or d << 16:
+// a half never carries, because the table is flushed before any candidate's
+// count can pass 63 spans x 1024 points), so the table fits beside the LDS
+// copy of the span's points.
+#ifndef SFM_MF2_TBL
+#define SFM_MF2_TBL 1
+#endif
+// the float64 drain reads its points from global memory (L2) instead of an LDS
+// copy of the span: the 32 KB make room for the count table
+#ifndef SFM_MF2_GPTS
+#define SFM_MF2_GPTS (SFM_MF2_TBL == 1)
 #endif
 #ifndef SFM_MF2_FOLD
 #define SFM_MF2_FOLD 1
@@ -76,9 +91,19 @@ constexpr int kMf2Waves = SFM_MF2_WAVES;       // 12: 3 per SIMD, two accumulato
 constexpr int kMf2Wpe = kMf2Waves / 4;
 constexpr int kMf2Span = SFM_MF2_SPAN;         // points per staged span
 constexpr int kMf2Tiles = kMf2Span / 32;       // tiles per span (every run decides all of them)
-constexpr int kMf2Queue = kMf2Waves > 12 ? 256 : 512;   // undecided entries per wave and drain window (LDS)
+#ifndef SFM_MF2_QLEN
+#define SFM_MF2_QLEN (SFM_MF2_TBL == 2 ? 128 : (SFM_MF2_TBL || SFM_MF2_WAVES > 12) ? 256 : 512)
+#endif
+#ifndef SFM_MF2_TBLCAP
+#define SFM_MF2_TBLCAP (SFM_MF2_TBL == 2 ? 352 : 384)
+#endif
+constexpr int kMf2Queue = SFM_MF2_QLEN;        // undecided entries per wave and drain window (LDS)
+// candidate tiles the LDS count table holds (tiles past it publish per run)
+constexpr int kMf2TblTiles = SFM_MF2_TBL ? SFM_MF2_TBLCAP : 1;
+constexpr int kMf2TblWords = SFM_MF2_TBL == 2 ? kMf2TblTiles * kKC / 2 : kMf2TblTiles * kKC;
+constexpr int kMf2TblSpans = 63;               // TBL 2: spans between flushes (63 x 1024 < 2^16)
+static_assert(SFM_MF2_TBL != 2 || kMf2Span <= 1024, "16-bit table counts");
 static_assert(kMf2Tiles <= 32 && kMf2Tiles % 2 == 0, "32-bit decision strings, tiles in pairs");
-static_assert(!SFM_MF2_CARRY || kMf2Span == 1024, "carried queue entries hold a 10-bit point");
 
 #ifdef SFM_MF_STATS
 // experiment builds only: [0] undecided evaluations, [1] evaluations decided by the tile loop
@@ -105,29 +130,21 @@ __device__ __forceinline__ void mf2_drain(const double* __restrict__ Erow0, cons
   }
 }
 
-// SFM_MF2_CARRY: the queue outlives the run.  Entries carry their candidate
-// tile (k << 15 | row << 10 | span-relative point), each run drains only
-// whole 64-entry rounds and keeps the rest for the next run of the same span
-// (the span's points stay staged), and inliers go straight to the pair's
-// global counts.  A run has ~67 undecided evaluations at the bench threshold
-// (0.2 %), so the per-run drain took two rounds, the second nearly empty.
-// Measured slower and off by default (profiles/r03_mf2_carry_ab.txt: 5.93-5.97
-// vs 5.71-5.75 ms): the drain's global atomics sit in the wave's vmcnt queue
-// ahead of the next run's A-row loads, so the prefetch wait grew by more
-// (stamps 2.2 -> 6.4 %) than the drain shrank (11.7 -> 4.7 %).
-__device__ __forceinline__ void mf2_drain_g(const double* __restrict__ Eb, const double4* __restrict__ spts,
-                                            const ScoreConsts& kc, int lane, int32_t* __restrict__ cT,
-                                            int32_t* __restrict__ cR, const uint32_t* q, int qn) {
+// The same test with each entry's point read from global memory (SFM_MF2_GPTS;
+// the span's points are L2-resident: the block staged them from there)
+template <class Src>
+__device__ __forceinline__ void mf2_drain_src(const double* __restrict__ Erow0, const Src& src, int b, int p0,
+                                              const ScoreConsts& kc, int lane, int32_t* cnt, const uint32_t* q,
+                                              int qn) {
 #pragma unroll 1
   for (int i = lane; i < qn; i += 64) {
     const uint32_t e = q[i];
-    const int c = (int)(e >> 15) * kKC + (int)((e >> 10) & 31u), r = (int)(e & 1023u);
-    if (inlier_f64v(Eb + (size_t)c * kCandStride, spts[r], kc)) {
-      atomicAdd(cT + c, 1);
-      atomicAdd(cR + c, 1);
-    }
+    const int c = (int)(e >> 24), r = (int)(e & 0xffffffu);
+    if (inlier_f64v(Erow0 + (size_t)c * kCandStride, src.load(b, (int64_t)p0 + r), kc)) atomicAdd(&cnt[c], 1);
   }
 }
+// (Round 3 measured a queue carried across runs, SFM_MF2_CARRY, and dropped
+// it: profiles/r03_mf2_carry_ab.txt.)
 
 // mf_tile_decide with each register's decisions kept together (scheduling
 // barriers): the compiler otherwise hoists all 32 FMAs of a tile ahead of the
@@ -232,9 +249,16 @@ template <class Src>
 __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(kMf2Wpe, kMf2Wpe))) void k_score_mf2(
     const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
     const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
-    int32_t* __restrict__ cntR, ScoreConsts kc, unsigned long long* __restrict__ claim) {
+    ScoreConsts kc, unsigned long long* __restrict__ claim) {
+  // one count array: this kernel runs only when num_test == num_ransac_test,
+  // so the preselection count is the score and k_select reads cntT for both
   __shared__ __attribute__((aligned(16))) _Float16 s_frag[kMf2Tiles][3][64][8];
+#if !SFM_MF2_GPTS
   __shared__ double4 s_pts[kMf2Span];
+#endif
+#if SFM_MF2_TBL
+  __shared__ int32_t s_tbl[kMf2TblWords];                    // the block's counts of pair tb's candidates
+#endif
   __shared__ uint32_t s_queue[kMf2Waves][kMf2Queue];
   __shared__ int32_t s_cnt[kMf2Waves][kKC];                  // float64 drain counts
   __shared__ long long s_first[SFM_MAX_BATCH + 1];           // first unit of each pair
@@ -257,6 +281,34 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     s_first[batch] = acc;
   }
   for (int i = tid; i < kMf2Waves * kKC; i += kMf2Waves * 64) (&s_cnt[0][0])[i] = 0;
+#if SFM_MF2_TBL
+  for (int i = tid; i < kMf2TblWords; i += kMf2Waves * 64) s_tbl[i] = 0;
+  int tb = -1;                                               // the pair the table holds (block-uniform)
+  int tspans = 0;                                            // spans added since the last flush
+  // the table to pair fb's global counts (all threads, between block barriers)
+  auto flush = [&](int fb) {
+    const int nt = min(s_tiles[fb], kMf2TblTiles) * kKC;
+    int32_t* dst = cntT + (size_t)fb * cmax;
+    if (SFM_MF2_TBL == 2) {
+      for (int i = tid; i < nt / 2; i += kMf2Waves * 64) {
+        const uint32_t v = (uint32_t)s_tbl[i];
+        if (v) {
+          if (v & 0xffffu) atomicAdd(dst + 2 * i, (int)(v & 0xffffu));
+          if (v >> 16) atomicAdd(dst + 2 * i + 1, (int)(v >> 16));
+          s_tbl[i] = 0;
+        }
+      }
+    } else {
+      for (int i = tid; i < nt; i += kMf2Waves * 64) {
+        const int v = s_tbl[i];
+        if (v) {
+          atomicAdd(dst + i, v);
+          s_tbl[i] = 0;
+        }
+      }
+    }
+  };
+#endif
   __syncthreads();
 #ifdef SFM_MF2_BLOCKT
   const unsigned long long blk_t0 = __builtin_amdgcn_s_memrealtime();
@@ -282,9 +334,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   const int logical = (G % 8 == 0) ? (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const long long u_beg = U * logical / G, u_end = U * (logical + 1) / G;
 #endif
-#if !SFM_MF2_CARRY
   int32_t* cnt = s_cnt[wv];
-#endif
   uint32_t* queue = s_queue[wv];
   const _Float16* fr = &s_frag[0][0][0][0];
   constexpr int kTileHalves = 3 * 64 * 8;
@@ -393,12 +443,24 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     const int k1 = (int)min((long long)tiles, (long long)k0 + (u_end - u));   // this block's tiles of the span
     const int p0 = span * kMf2Span;
     const int np = min(max(pp.test[b], pp.rtest[b]) - p0, kMf2Span);     // live points of the span
+#if SFM_MF2_TBL
+    // a new pair: the table's counts go out first (every wave's adds to it
+    // ended before the barrier that closed the previous span or claim)
+    if (b != tb || (SFM_MF2_TBL == 2 && tspans == kMf2TblSpans)) {
+      if (tb >= 0) flush(tb);
+      tb = b;
+      tspans = 0;
+    }
+    ++tspans;
+#endif
     // 1. stage the span: B fragments for every slot (dead slots: the decided-outlier sentinel)
     if (tid == 0) s_claim = 0;
     for (int i = tid; i < kMf2Span; i += kMf2Waves * 64) {
       const bool live = i < np;
       const double4 v = src.load(b, live ? p0 + i : p0);
+#if !SFM_MF2_GPTS
       s_pts[i] = v;
+#endif
       mf_stage_point(v, live, &s_frag[i >> 5][0][0][0], i & 31);
     }
     MF_STAMP(0);
@@ -416,12 +478,6 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     int k = claim();
     const int ctot = __builtin_amdgcn_readfirstlane(s_ctot[b]);   // the pair's candidates, in an SGPR
     if (k < k1) load_rows(b, k, ctot);
-#if SFM_MF2_CARRY
-    int qn = 0;                                               // carried queue entries (wave-uniform)
-    const double* Eb = candE + (size_t)b * cmax * kCandStride;
-    int32_t* cTb = cntT + (size_t)b * cmax;
-    int32_t* cRb = cntR + (size_t)b * cmax;
-#endif
 #pragma unroll 1
     while (k < k1) {
 #ifdef SFM_MF_STAMPS
@@ -557,59 +613,6 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         atomicAdd(&g_mf2_stats[1], (unsigned long long)kKC * kMf2Span);
       }
 #endif
-#if SFM_MF2_CARRY
-      if (qn + qtotal <= kMf2Queue) {
-        uint32_t* q = queue + qn + (incl - nl);
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          uint32_t uu = mf2_undecided(s1[g], s2[g]);
-          const uint32_t top = ((uint32_t)k << 15) | ((uint32_t)mf_row(g, hl) << 10) |
-                               (uint32_t)(32 * (kMf2Tiles - 1) + rl);
-          while (uu) {
-            *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
-            uu &= uu - 1u;
-          }
-        }
-        qn += qtotal;
-        wave_sync();
-        MF_STAMP(2);
-        if (qn >= 64) {
-          const int nd = qn & ~63;
-          mf2_drain_g(Eb, s_pts, kc, lane, cTb, cRb, queue, nd);
-          uint32_t keep = 0u;
-          if (lane < qn - nd) keep = queue[nd + lane];
-          wave_sync();
-          if (lane < qn - nd) queue[lane] = keep;
-          wave_sync();
-          qn -= nd;
-        }
-        MF_STAMP(3);
-      } else {
-        // more than the queue holds: drain the carry, then this run in windows
-        mf2_drain_g(Eb, s_pts, kc, lane, cTb, cRb, queue, qn);
-        qn = 0;
-        wave_sync();
-        for (int base = 0; base < qtotal; base += kMf2Queue) {
-          int pos = incl - nl - base;
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            uint32_t uu = mf2_undecided(s1[g], s2[g]);
-            const uint32_t top = ((uint32_t)k << 15) | ((uint32_t)mf_row(g, hl) << 10) |
-                                 (uint32_t)(32 * (kMf2Tiles - 1) + rl);
-            while (uu) {
-              if (pos >= 0 && pos < kMf2Queue) queue[pos] = top - 32u * (uint32_t)__builtin_ctz(uu);
-              uu &= uu - 1u;
-              ++pos;
-            }
-          }
-          wave_sync();
-          MF_STAMP(2);
-          mf2_drain_g(Eb, s_pts, kc, lane, cTb, cRb, queue, min(kMf2Queue, qtotal - base));
-          wave_sync();
-          MF_STAMP(3);
-        }
-      }
-#else
       const double* Erow0 = candE + ((size_t)b * cmax + c0) * kCandStride;
       for (int base = 0; base < qtotal; base += kMf2Queue) {
         int pos = incl - nl - base;
@@ -665,12 +668,15 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         }
         wave_sync();
         MF_STAMP(2);
+#if SFM_MF2_GPTS
+        mf2_drain_src(Erow0, src, b, p0, kc, lane, cnt, queue, min(kMf2Queue, qtotal - base));
+#else
         mf2_drain(Erow0, s_pts, kc, lane, cnt, queue, min(kMf2Queue, qtotal - base));
+#endif
         wave_sync();
         MF_STAMP(3);
       }
       MF_STAMP(2);
-#endif
       // 4. counts: popcounts of the inlier strings over the 32 points of each half + the float64 counts
       int cT[16];
 #pragma unroll
@@ -678,33 +684,35 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       const int sumT = mf_half_reduce(cT, lane);
       if ((lane & 1) == 0) {
         const int c = mf_row((rl >> 1) & 15, hl);
-#if SFM_MF2_CARRY
-        const int d = sumT;
-#else
         const int d = sumT + cnt[c];
         cnt[c] = 0;
-#endif
         if (d && c0 + c < ctot) {
-          atomicAdd(cntT + (size_t)b * cmax + c0 + c, d);
-          atomicAdd(cntR + (size_t)b * cmax + c0 + c, d);
+#if SFM_MF2_TBL
+          if (k < kMf2TblTiles) {
+            if (SFM_MF2_TBL == 2)                             // two candidates per word: an LDS atomic
+              atomicAdd(&s_tbl[(c0 + c) >> 1], d << (16 * ((c0 + c) & 1)));
+            else
+              s_tbl[c0 + c] += d;                             // tile k of this span is this wave's alone
+          } else
+#endif
+            atomicAdd(cntT + (size_t)b * cmax + c0 + c, d);
         }
       }
       wave_sync();
       MF_STAMP(4);
       k = kn;
     }
-#if SFM_MF2_CARRY
-    if (qn) {                                                 // the span's last entries, before it is re-staged
-      mf2_drain_g(Eb, s_pts, kc, mf2_lane(), cTb, cRb, queue, qn);
-      wave_sync();
-    }
-#endif
     u += k1 - k0;
     lds_barrier();                                            // the span is re-staged next
     MF_STAMP(5);
   }
 #if SFM_MF2_DYN
   }
+#endif
+#if SFM_MF2_TBL
+  // (DYN: the loop left right after a block barrier; static ranges: after the
+  // last span's barrier)
+  if (tb >= 0) flush(tb);
 #endif
 #if SFM_MF2_DYN
   // the last block out zeroes the counters (claim[8] counts finished blocks),

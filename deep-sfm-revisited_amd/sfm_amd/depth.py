@@ -53,8 +53,10 @@ def correlation_cost(ref_fea, tgt_fea, pose, intrinsics4, intrinsics_inv4, nlabe
     return out
 
 
-def depth_head(cost, nlabel, min_depth=1.0, out_hw=None, predict_by_depth=False, out=None):
-    """Soft-argmin depth [B, 1, H, W] float32 from a cost [B, L, h, w] / [B, 1, L, h, w]."""
+def depth_head(cost, nlabel, min_depth=1.0, out_hw=None, predict_by_depth=False, out=None, scale=None):
+    """Soft-argmin depth [B, 1, H, W] float32 from a cost [B, L, h, w] / [B, 1, L, h, w].
+    ``scale`` (predict_by_depth only) replaces the final ``* min_depth``: PSNet's
+    depth_init is depthregression's output without it (PSNet.py:200-202)."""
     c = _dev_f32(cost, "cost")
     if c.dim() == 5:
         if c.shape[1] != 1:
@@ -72,8 +74,9 @@ def depth_head(cost, nlabel, min_depth=1.0, out_hw=None, predict_by_depth=False,
     if out is None:
         out = torch.empty(B, 1, H, W, dtype=torch.float32, device=c.device)
     with torch.cuda.device(c.device):
+        mul = float(min_depth) if (scale is None or not predict_by_depth) else float(scale)
         rc = _lib.load().sfm_depth_head(_lib.ptr(c), B, L, h, w, H, W, 1 if predict_by_depth else 0,
-                                        float(min_depth), step, _lib.ptr(out), _lib.stream_ptr(c.device))
+                                        mul, step, _lib.ptr(out), _lib.stream_ptr(c.device))
         _lib.check(rc, "sfm_depth_head")
     return out
 

@@ -109,10 +109,13 @@ class PSNet(CostRegularization):
 
     ``feature_fn`` replaces the feature CNN (any callable image -> [B, 32,
     H/4, W/4]); ``conv_precision`` selects the regularisation arithmetic
-    (CostRegularization); ``cost_dtype`` the sweep volume's storage."""
+    (CostRegularization): "fp32" (default) is the reference's own precision
+    (PSNet.py:159-165 in float32; its MIXED_PREC autocast would run fp16, whose
+    mantissa is still wider than bf16's), "bf16" the faster opt-in path;
+    ``cost_dtype`` the sweep volume's storage."""
 
     def __init__(self, nlabel, mindepth=None, cfg=None, feature_fn=None, cost_dtype=torch.float32,
-                 conv_precision="bf16"):
+                 conv_precision="fp32"):
         super().__init__(64)
         c = _default_cfg if cfg is None else cfg
         if c.get("COST_BY_COLOR", False) or c.get("COST_BY_COLOR_WITH_FEAT", False):
@@ -159,12 +162,17 @@ class PSNet(CostRegularization):
         H, W = ref.shape[2], ref.shape[3]
         costss = costs
         if c.get("PSNET_CONTEXT", True):
-            ctx = self.context_net(ref).float() if c.get("IND_CONTEXT", False) else ref_fea
+            if c.get("IND_CONTEXT", False):
+                ref_fea = self.context_net(ref).float()        # PSNet.py:177-178 reassigns refimg_fea
+            ctx = ref_fea
             # every plane through the same 2-D stack: one batch of B*L images
             planes = costs[:, 0].permute(1, 0, 2, 3).reshape(L * B, 1, h, w)
             x = torch.cat([ctx.unsqueeze(0).expand(L, B, ctx.shape[1], h, w).reshape(L * B, -1, h, w), planes], 1)
             costss = (self.convs(x) + planes).reshape(L, B, h, w).permute(1, 0, 2, 3).unsqueeze(1)
-        depth_init = depth_head(costs.reshape(B, L, h, w).contiguous(), self.nlabel, self.mindepth, (H, W), pbd)
+        # PREDICT_BY_DEPTH: depth_init is depthregression's output unscaled,
+        # depth is scaled by mindepth (PSNet.py:200-202 vs 209-210)
+        depth_init = depth_head(costs.reshape(B, L, h, w).contiguous(), self.nlabel, self.mindepth, (H, W), pbd,
+                                scale=1.0 if pbd else None)
         depth = depth_head(costss.reshape(B, L, h, w).contiguous(), self.nlabel, self.mindepth, (H, W), pbd)
         if c.get("PSNET_DEP_CONTEXT", False):
             up = F.interpolate(ref_fea, [H, W], mode="bilinear", align_corners=True)

@@ -89,25 +89,30 @@ class score_precision:
     C5's fp32-vs-fp16 sweep).  Nests: leaving restores the precision that was
     in force on entry.  Not thread-safe across concurrent callers.
 
-    The 32 / 16 arithmetic is this build's variant of the reference's template
-    (kernel_functions.cu:231-264), which is only ever instantiated with
-    T = double there: here E, the products and the sums are all held in T
-    (see DESIGN.md "Reduced-precision scoring"); its parity is unpinned by any
-    reference output."""
+    The reference only ever instantiates its template (kernel_functions.cu:
+    231-264) with T = double, so both reduced forms are parity-unpinned
+    against the reference (see DESIGN.md "Reduced-precision scoring"):
+      * 32 / 16: this build's variant, E, the products and the sums all held
+        in T (E normalised by a power of two);
+      * 33 / 17: the literal ComputeError<float> / <half> with the reference's
+        double Ematrix (common.h:26): double products, sums rounded to T."""
 
     def __init__(self, bits):
-        if int(bits) not in (64, 32, 16):
-            raise ValueError("score precision must be 64, 32 or 16")
+        if int(bits) not in (64, 32, 16, 33, 17):
+            raise ValueError("score precision must be 64, 32, 16 (held in T) or 33, 17 (template form)")
         self.bits = int(bits)
         self._saved = []
 
     def __enter__(self):
-        self._saved.append(int(_lib.tune_get("score_precision")))
-        _lib.tune("score_precision", self.bits)
+        self._saved.append((int(_lib.tune_get("score_precision")), int(_lib.tune_get("score_lowp_template"))))
+        _lib.tune("score_precision", self.bits & ~1 if self.bits != 64 else 64)
+        _lib.tune("score_lowp_template", self.bits & 1)
         return self
 
     def __exit__(self, *exc):
-        _lib.tune("score_precision", self._saved.pop())
+        p, t = self._saved.pop()
+        _lib.tune("score_precision", p)
+        _lib.tune("score_lowp_template", t)
 
 
 def ransac5_batched(pts, n=None, num_test_points=None, num_ransac_test_points=None, iters=5, threshold=1e-4,

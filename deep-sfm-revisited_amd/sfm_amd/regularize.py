@@ -9,10 +9,10 @@ its application at PSNet.py:159-165:
     cost0 = classify(cost0)                      # [B, 1, L, h, w]
 
 ``CostRegularization.forward`` runs the 12 Conv3d layers as
-``sfm_conv3_bf16`` launches (bf16 channels-last activations, fp32
-accumulation; the fast option) or, with ``precision="fp32"``, as
-``sfm_conv3_f32`` launches (fp32 activations and weights on the f32 matrix
-cores: the reference's precision).  BatchNorm3d is folded in eval mode, ReLU
+``sfm_conv3_f32`` launches (default ``precision="fp32"``: fp32 activations
+and weights on the f32 matrix cores, the reference's precision) or, with
+``precision="bf16"``, as ``sfm_conv3_bf16`` launches (bf16 channels-last
+activations, fp32 accumulation; the fast opt-in option).  BatchNorm3d is folded in eval mode, ReLU
 and residual are fused into the epilogue.  There is no PyTorch fallback: without libsfm_hip.so or a GPU
 the call raises.
 """
@@ -143,11 +143,12 @@ class CostRegularization(nn.Module):
         self._packed, self._packed_key = packed, key
         return packed
 
-    def forward(self, cost, precision="bf16"):
+    def forward(self, cost, precision="fp32"):
         """cost [B, Cin, L, h, w] fp32 or bf16 (the sweep's volume) -> [B, 1, L, h, w] fp32.
-        ``precision``: "bf16" (bf16 activations and weights, fp32 accumulation:
-        sfm_conv3_bf16, the fast option) or "fp32" (fp32 activations, weights
-        and accumulation: sfm_conv3_f32, the reference's precision)."""
+        ``precision``: "fp32" (default: fp32 activations, weights and
+        accumulation, sfm_conv3_f32, the reference's precision) or "bf16" (bf16
+        activations and weights, fp32 accumulation: sfm_conv3_bf16, the fast
+        opt-in)."""
         if precision not in ("bf16", "fp32"):
             raise ValueError(f"unknown conv precision {precision!r}")
         if not (isinstance(cost, torch.Tensor) and cost.is_cuda):

@@ -387,7 +387,13 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *     "score_precision"       64, 32, 16  64 (default): the reference's float64
  *                                     ComputeError decision, exact; 32 / 16:
  *                                     ComputeError<float> / <half> semantics
- *                                     (approximate inlier sets, BASELINE C5) */
+ *                                     (approximate inlier sets, BASELINE C5)
+ *     "score_lowp_template"   0, 1    32 / 16 only: 0 (default) E and every
+ *                                     operation held in T; 1 the literal
+ *                                     ComputeError<T> with the reference's
+ *                                     double Ematrix (double products, sums
+ *                                     rounded to T; kernel_functions.cu:231-264,
+ *                                     common.h:26) */
 int sfm_tune_set(const char* key, int value);
 /* The current value of a tuning key. */
 int sfm_tune_get(const char* key, int* value);

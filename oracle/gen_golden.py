@@ -21,6 +21,8 @@ Run in the survey container, where /root/reference exists:
   submodule.py) at seed 0 on a reduced 128x192 pair, nlabel 16, eval mode with
   seeded BatchNorm3d statistics; forward hooks record the features, the cost
   volume, the classify output and the soft-argmin depth (depth_init).
+* psnet64.npz: the same reference PSNet run in float64 and in float32 on the
+  same (unit-scale) features: the exact depth the fp32 product path is held to.
 
 Only inputs and outputs are written (no reference source).
 """
@@ -443,6 +445,109 @@ def gen_psnet():
     return out
 
 
+class _FixedFeatures(torch.nn.Module):
+    """Stands in for PSNet.feature_extraction: returns the given feature maps
+    in call order (ref, then the target), in the dtype of the image it gets."""
+
+    def __init__(self, feas):
+        super().__init__()
+        self.feas, self.i = feas, 0
+
+    def forward(self, img):
+        f = self.feas[self.i % len(self.feas)].to(img.dtype)
+        self.i += 1
+        return f
+
+
+class _Float64:
+    """The reference PSNet in float64: default dtype float64 (torch.ones /
+    torch.Tensor buffers) and torch.FloatTensor(...) -- the cost-volume buffer
+    of PSNet.py:146 -- allocating float64, for the duration of the block."""
+
+    def __enter__(self):
+        self.dt, self.ft = torch.get_default_dtype(), torch.FloatTensor
+        torch.set_default_dtype(torch.float64)
+        torch.FloatTensor = lambda *size: torch.zeros(*size, dtype=torch.float64)
+        return self
+
+    def __exit__(self, *a):
+        torch.set_default_dtype(self.dt)
+        torch.FloatTensor = self.ft
+
+
+def gen_psnet64():
+    """The depth bar's exact answer (VERDICT r03 'Next' #2): the reference PSNet
+    (PSNET_CONTEXT off, RESCALE_DEPTH, as psnet.npz) run in float64 and in
+    float32 on the SAME float32 feature maps and the same float32-valued
+    weights.  The features are psnet.npz's random-init network output scaled to
+    unit standard deviation, and the classify layer is scaled so the float64
+    logits have standard deviation 4 (a trained net's regime), so the fixture
+    measures arithmetic error rather than a random-init net's amplification of
+    1-ulp input changes.  depth64 is the exact reference; depth32 is the
+    reference's own float32 error against it."""
+    import copy
+    import sys
+    B, H, W, L = 1, 128, 192, 16
+    out = {}
+    with _RefEnv() as env:
+        cfg = env.import_("lib.config").cfg
+        cfg.update(PSNET_CONTEXT=False, RESCALE_DEPTH=True, NORM_TARGET=0.8)
+        PS = env.import_("models.PSNet")
+        torch.manual_seed(0)
+        net = PS.PSNet(L, 1.0)
+        g = torch.Generator().manual_seed(5)
+        for mod in net.modules():
+            if isinstance(mod, torch.nn.BatchNorm3d):
+                c = mod.num_features
+                mod.running_mean.copy_(0.1 * torch.randn(c, generator=g))
+                mod.running_var.copy_(0.5 + torch.rand(c, generator=g))
+                mod.weight.data.copy_(0.8 + 0.4 * torch.rand(c, generator=g))
+                mod.bias.data.copy_(0.1 * torch.randn(c, generator=g))
+        net.eval()
+        ref = torch.rand(B, 3, H, W, generator=g) * 2 - 1
+        tgt = torch.rand(B, 3, H, W, generator=g) * 2 - 1
+        K = torch.tensor([[[100.0, 0, 95.5], [0, 98.0, 63.5], [0, 0, 1]]])
+        Kinv = torch.inverse(K)
+        a = torch.tensor([[0, -0.02, 0.01], [0.02, 0, -0.015], [-0.01, 0.015, 0.0]])
+        pose = torch.cat([torch.matrix_exp(a), torch.tensor([[0.2], [-0.05], [-1.2]])], 1).reshape(1, 1, 3, 4)
+        with torch.no_grad():
+            feas = [net.feature_extraction(x) for x in (ref, tgt)]
+            feas = [(f / f.std()).float() for f in feas]
+        net.feature_extraction = _FixedFeatures(feas)
+        iw = sys.modules["models.inverse_warp"]
+        rec = {}
+        net.classify.register_forward_hook(lambda m, i, o: rec.__setitem__("classify", o.detach().clone()))
+        net.dres0.register_forward_pre_hook(lambda m, i: rec.__setitem__("cost", i[0].detach().clone()))
+
+        def run(dtype):
+            m = copy.deepcopy(net).to(dtype)
+            m.feature_extraction.i = 0
+            iw.pixel_coords = None                        # its id-grid cache keeps the first call's dtype
+            with torch.no_grad():
+                if dtype == torch.float64:
+                    with _Float64():
+                        r = m(ref.double(), [tgt.double()], pose.clone().double(), K.double(), Kinv.double())
+                else:
+                    r = m(ref, [tgt], pose.clone(), K, Kinv)
+            return [t.clone() for t in r], rec["classify"], rec["cost"]
+        _, cls64, _ = run(torch.float64)
+        with torch.no_grad():                             # float32 weights, so both runs use the same values
+            net.classify[2].weight.mul_(float(4.0 / cls64.std()))
+        (di64, d64), cls64, _ = run(torch.float64)
+        (di32, d32), cls32, _ = run(torch.float32)
+        state = {k: v.numpy() for k, v in net.state_dict().items()
+                 if k.startswith("dres") or k.startswith("classify")}
+        pose_rescaled = pose.clone()
+        pose_rescaled[:, 0, :, -1:] = pose_rescaled[:, 0, :, -1:] * 0.8
+    out["input"] = dict(ref_fea=feas[0].numpy(), tgt_fea=feas[1].numpy(), K=K.numpy(), Kinv=Kinv.numpy(),
+                        pose=pose.numpy(), pose_rescaled=pose_rescaled.numpy(), nlabel=np.int32(L),
+                        min_depth=np.float32(1.0), image_hw=np.array([H, W], np.int32))
+    out["out64"] = dict(depth=d64.numpy(), depth_init=di64.numpy(), classify=cls64.numpy())
+    out["out32"] = dict(depth=d32.numpy(), depth_init=di32.numpy(), classify=cls32.numpy())
+    out["state"] = state
+    return out
+
+
 def gen_psnet_keys():
     """state_dict key -> shape of the reference PSNet as SFMnet builds it by
     default (SFMnet.py:57-58) with cfgs/kitti.yml's PSNET_DEP_CONTEXT: pins
@@ -472,7 +577,7 @@ def main(argv=None):
     """python -m oracle.gen_golden [name ...]  (default: every fixture)."""
     import sys
     want = set((sys.argv[1:] if argv is None else argv) or
-               ["solve5", "ransac", "irls", "sampler", "warp", "corr", "psnet", "psnet_keys"])
+               ["solve5", "ransac", "irls", "sampler", "warp", "corr", "psnet", "psnet64", "psnet_keys"])
     os.makedirs(OUT, exist_ok=True)
     rng = np.random.default_rng(20241015)
     # the rng is consumed in this order, so a subset regenerates identical files
@@ -489,6 +594,8 @@ def main(argv=None):
         _save("corr.npz", gen_corr())
     if "psnet" in want:
         _save("psnet.npz", gen_psnet())
+    if "psnet64" in want:
+        _save("psnet64.npz", gen_psnet64())
     if "psnet_keys" in want:
         import json
         path = os.path.join(OUT, "psnet_keys.json")

@@ -122,6 +122,7 @@ def ransac5(q, qp, num_test=None, num_ransac_test=None, iters=5, thr=1e-4, seed=
             nchains=512, nthreads=0, use_ref=False, prec=64):
     """Full RANSAC emulation for one pair. Returns dict(E, P, inliers, winner,
     hyp_score, hyp_ncand).  prec: 64 (the reference's ComputeError<double>),
+    33 / 17 (the literal ComputeError<float> / <half> template form),
     32 / 16 (ComputeError<float> / <half>, ransac5_oracle.cpp:is_inlier_lp)."""
     q = np.ascontiguousarray(q, dtype=np.float64)
     qp = np.ascontiguousarray(qp, dtype=np.float64)
@@ -181,6 +182,38 @@ def inlier_mask_numpy(E, q, qp, thr, prec):
         D = ((ex0 * ex0 + ex1 * ex1) + xe0 * xe0) + xe1 * xe1
         d = np.sqrt(D.astype(np.float32)).astype(T)
         err = np.abs((a.astype(np.float32) / d.astype(np.float32)).astype(T))
+    return err.astype(np.float64) <= thr
+
+
+def inlier_mask_numpy_tpl(E, q, qp, thr, prec):
+    """numpy restatement of ransac5_oracle.cpp:is_inlier_lp_tpl (prec 33 = float,
+    17 = half): the literal ComputeError<T> with a double Ematrix (double
+    products and adds, each sum rounded to T; xEx, D, sqrt, division in T).
+    numpy's float64 -> float16 conversion rounds once, like h16d."""
+    T = np.float16 if prec == 17 else np.float32
+    E = np.asarray(E, np.float64).reshape(3, 3)
+    q = [np.asarray(q[:, 0], np.float64).astype(T), np.asarray(q[:, 1], np.float64).astype(T),
+         np.ones(len(q), T)]
+    qp = [np.asarray(qp[:, 0], np.float64).astype(T), np.asarray(qp[:, 1], np.float64).astype(T),
+          np.ones(len(qp), T)]
+    with np.errstate(all="ignore"):
+        Ex, xE = [], []
+        for k in range(3):
+            s_ = np.zeros(len(q[0]), T)
+            for l in range(3):
+                s_ = (s_.astype(np.float64) + E[k, l] * q[l].astype(np.float64)).astype(T)
+            Ex.append(s_)
+        for k in range(3):
+            s_ = np.zeros(len(q[0]), T)
+            for l in range(3):
+                s_ = (s_.astype(np.float64) + qp[l].astype(np.float64) * E[l, k]).astype(T)
+            xE.append(s_)
+        xEx = np.zeros(len(q[0]), T)
+        for k in range(3):
+            xEx = xEx + qp[k] * Ex[k]
+        D = ((Ex[0] * Ex[0] + Ex[1] * Ex[1]) + xE[0] * xE[0]) + xE[1] * xE[1]
+        d = np.sqrt(D.astype(np.float32)).astype(T)
+        err = np.abs((xEx.astype(np.float32) / d.astype(np.float32)).astype(T))
     return err.astype(np.float64) <= thr
 
 

@@ -689,9 +689,60 @@ static inline bool is_inlier_lp(const double* E, double xd, double yd, double xp
   return (double)err <= thr;
 }
 
+// A double rounded once to binary16 (ties to even; subnormals; overflow to
+// inf), returned as a double.  The quantum arithmetic is exact in double.
+static inline double h16d(double v) {
+  if (!(std::fabs(v) < 65520.0)) return (double)h16((float)v);
+  const double a = std::fabs(v);
+  double q;
+  if (a < 0x1p-14) {
+    q = 0x1p-24;
+  } else {
+    int e;
+    std::frexp(a, &e);
+    q = std::ldexp(1.0, e - 1 - 10);
+  }
+  return std::copysign(std::nearbyint(a / q) * q, v);
+}
+
+// The literal ComputeError<T> (kernel_functions.cu:231-264) with the
+// reference's Ematrix = double[3][3] (common.h:26), T = float (prec 33) or
+// binary16 (prec 17): q, qp converted to T once; `sum += E[k][l] * q[l]` is a
+// double product and a double add, the sum rounded to T; xEx, D, sqrt and the
+// division in T (half: computed in float, rounded once -- exact by the
+// 24 >= 2*11+2 rule); no scaling of E.  Mirrors ransac5.hip:inlier_lowp_tpl.
+template <int PREC>
+static inline bool is_inlier_lp_tpl(const double* E, double xd, double yd, double xpd, double ypd, double thr) {
+  auto rd = [](double v) { return PREC == 17 ? h16d(v) : (double)(float)v; };     // double -> T
+  auto r = [](float v) { return PREC == 17 ? h16(v) : v; };                      // float op result -> T
+  const double q[3] = {rd(xd), rd(yd), 1.0}, qp[3] = {rd(xpd), rd(ypd), 1.0};
+  float Ex[3], xE[3];
+  for (int k = 0; k < 3; ++k) {
+    double sum = 0.0;
+    for (int l = 0; l < 3; ++l) sum = rd(sum + E[3 * k + l] * q[l]);
+    Ex[k] = (float)sum;
+  }
+  for (int k = 0; k < 3; ++k) {
+    double sum = 0.0;
+    for (int l = 0; l < 3; ++l) sum = rd(sum + qp[l] * E[3 * l + k]);
+    xE[k] = (float)sum;
+  }
+  float xEx = 0.0f;
+  for (int k = 0; k < 3; ++k) xEx = r(xEx + r((float)qp[k] * Ex[k]));
+  float D = r(r(Ex[0] * Ex[0]) + r(Ex[1] * Ex[1]));
+  D = r(D + r(xE[0] * xE[0]));
+  D = r(D + r(xE[1] * xE[1]));
+  const float d = r(std::sqrt(D));
+  float err = r(xEx / d);
+  if (err < 0.0f) err = -err;
+  return (double)err <= thr;
+}
+
 static inline bool is_inlier_p(const double* E, double x, double y, double xp, double yp, double thr, int prec) {
   if (prec == 32) return is_inlier_lp<32>(E, x, y, xp, yp, thr);
   if (prec == 16) return is_inlier_lp<16>(E, x, y, xp, yp, thr);
+  if (prec == 33) return is_inlier_lp_tpl<33>(E, x, y, xp, yp, thr);
+  if (prec == 17) return is_inlier_lp_tpl<17>(E, x, y, xp, yp, thr);
   return is_inlier(E, x, y, xp, yp, thr);
 }
 
@@ -761,12 +812,13 @@ void orc_inlier_mask_prec(const double* E, const double* q, const double* qp, in
 //   * if no hypothesis has > 0 inliers, E = P = 0, inliers = 0, winner = -1.
 // hyp_score (optional, nchains*iters): rescored inlier count per hypothesis.
 // hyp_ncand (optional): nP (cheir) / nroots (no cheir) per hypothesis.
-// prec: 64 = ComputeError<double> (the reference), 32 / 16 = is_inlier_lp.
+// prec: 64 = ComputeError<double> (the reference), 32 / 16 = is_inlier_lp,
+// 33 / 17 = is_inlier_lp_tpl (the literal template form).
 int orc_ransac5_prec(const double* q, const double* qp, int64_t n, int num_test, int num_ransac_test,
                      int nchains, int iters, double thr, uint64_t seed, int cheir, int nthreads, int prec,
                      double* E_out, double* P_out, int* inliers_out, int* winner_out,
                      int* hyp_score, int* hyp_ncand, int* hyp_best) {
-  if (prec != 64 && prec != 32 && prec != 16) return 1;
+  if (prec != 64 && prec != 32 && prec != 16 && prec != 33 && prec != 17) return 1;
   if (n < 1 || num_test < 0 || num_ransac_test < 0 || num_test > n || num_ransac_test > n) return 1;
   const int H = nchains * iters;
   std::vector<int> score(H, 0), best(H, 0);

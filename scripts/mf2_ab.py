@@ -4,7 +4,8 @@ N=435,032, H=4096): per-launch score time from libsfm_hip's HIP events,
 outputs (E, P, inliers, winner and the per-hypothesis score vector) must equal
 the first variant's bit for bit.  With a library built with -DSFM_MF_STATS
 (scripts/build_exp.sh) it also prints k_score_mf2's undecided fraction.
-Usage: mf2_ab.py "score_mf=1" "score_mf=2" ...   (SFM_HIP_LIB selects the library)"""
+Usage: mf2_ab.py "score_mf=1" "score_mf=2" ...   (SFM_HIP_LIB selects the library;
+AB_REF=file compares the outputs across libraries)"""
 import ctypes
 import os
 import sys
@@ -58,3 +59,14 @@ for i in range(len(variants)):
     print(f"{names[i] or 'default':30s} score median {r[len(r) // 2]:.3f} ms  all {[round(x, 3) for x in res[i]]}",
           flush=True)
 print("inliers", base[2].tolist())
+# across libraries: AB_REF=path saves the first library's outputs there, and
+# every later process compares its own with them bit for bit
+ref = os.environ.get("AB_REF")
+if ref:
+    if not os.path.exists(ref):
+        torch.save([t.cpu() for t in base], ref)
+    else:
+        want = torch.load(ref, weights_only=True)
+        for a, b in zip(want, base):
+            assert torch.equal(a, b.cpu()), "this library changed the output"
+        print("outputs equal the reference library's", flush=True)

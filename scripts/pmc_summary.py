@@ -92,9 +92,17 @@ def main(src, dst, config="c2"):
     json.dump({"source": "rocprofv3 --pmc --kernel-trace, separate passes (scripts/gpu_pmc.sh) over "
                          f"`python3 bench.py --config {config} --steps 1 --warmup 1 --no-cpu-baseline`",
                "workload": {"config": config, "batch": b, "nlabel": nl, "iters": it, "cost_dtype": cd},
+               "src_hash": _src_hash(),
                "kernels": out}, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps({k: {x: v.get(x) for x in ("hbm_read_bytes", "hbm_write_bytes", "l2_hit_rate")}
                       for k, v in out.items()}, indent=1))
+
+
+def _src_hash():
+    """bench.src_hash() of the sources in this tree (the ones the counters were recorded from)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    return bench.src_hash()
 
 
 if __name__ == "__main__":

@@ -41,14 +41,36 @@ def pytest_collection_modifyitems(session, config, items):
         return
     out = tempfile.mkdtemp(prefix="sfm_dist_")
     port = _free_port()
-    procs = []
+    procs, logs = [], []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", LOCAL_WORLD_SIZE="2",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SFM_DIST_OUT=out)
         log = open(os.path.join(out, f"rank{r}.log"), "w")
+        logs.append(log)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "helpers", "dist_gpu_worker.py")],
                                       env=env, stdout=log, stderr=subprocess.STDOUT))
+    for log in logs:          # the children hold their own descriptors
+        log.close()
     config._sfm_dist_ranks = (procs, out)
+
+
+def _stop_ranks(procs):
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except Exception:
+            pass
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """The dist ranks never outlive the session, whether or not their test ran
+    (e.g. an earlier failure under -x)."""
+    ranks = getattr(session.config, "_sfm_dist_ranks", None)
+    if ranks is not None:
+        _stop_ranks(ranks[0])
 
 
 def _free_port():
@@ -64,9 +86,7 @@ def dist_gpu_ranks(request):
     if ranks is None:
         pytest.skip("ranks not started (no GPU, or the test was not collected at session start)")
     yield ranks
-    for p in ranks[0]:
-        if p.poll() is None:
-            p.kill()
+    _stop_ranks(ranks[0])
 
 
 def load_golden(name):

@@ -36,7 +36,20 @@ def test_spawns_two_ranks_without_torchrun():
     assert out["config"]["pairs_per_gpu"] == 4 and out["config"]["global_batch"] == 8
     # every rank's pairs reach rank 0, in rank order
     assert out["gathered"]["pairs"] == 8
-    assert out["gathered"]["rows"] == [[float(r), float(i)] for r in range(2) for i in range(4)]
+    assert out["gathered"]["rows"] == [[float(r), float(r), float(i)] for r in range(2) for i in range(4)]
+
+
+def test_eight_rank_c3_shape():
+    """The driver's SCALE run at its real shape (BASELINE C3: 8
+    ranks x 4 bf16 pairs, embarrassingly data-parallel): 32 pairs gathered to
+    rank 0 in rank order, every rank driving the device of its LOCAL_RANK."""
+    r = _run(["--gpus", "8", "--steps", "2", "--warmup", "1", "--config", "c3"], timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = _json_line(r.stdout)
+    assert out["n_gpus"] == 8 and out["dist"]["world_size"] == 8
+    assert out["config"]["pairs_per_gpu"] == 4 and out["config"]["global_batch"] == 32
+    assert out["gathered"]["pairs"] == 32
+    assert out["gathered"]["rows"] == [[float(r), float(r), float(i)] for r in range(8) for i in range(4)]
 
 
 def test_single_rank_default():
@@ -65,10 +78,11 @@ def test_pmc_summaries_sort_numerically():
     assert bench._round_version("profiles/r01_conv_pmc.json") == (-1, -1)
 
 
-def test_pmc_traffic_matches_the_workload():
+def test_pmc_traffic_matches_the_workload(tmp_path, monkeypatch):
     """The bench line's `traffic` comes only from a PMC summary collected on the
-    same workload: c2 and c3 each find their own file, a config without one
-    reports none."""
+    same workload from the same sources (src_hash): c2 and c3 each
+    find their own file, a config without one reports none, and a newer
+    summary recorded from other sources is ignored."""
     import types
     sys.path.insert(0, ROOT)
     import bench
@@ -77,14 +91,36 @@ def test_pmc_traffic_matches_the_workload():
         b, _, it, nl, cd, _ = bench.CONFIGS[cfg]
         return types.SimpleNamespace(config=cfg, batch=batch or b, nlabel=nl, iters=it, cost_dtype=cd)
 
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+
+    def summary(name, cfg, h):
+        b, _, it, nl, cd, _ = bench.CONFIGS[cfg]
+        d = {"workload": {"config": cfg, "batch": b, "nlabel": nl, "iters": it, "cost_dtype": cd},
+             "kernels": {"ransac_score": {"hbm_bytes": 1}}}
+        if h:
+            d["src_hash"] = h
+        (prof / name).write_text(json.dumps(d))
+    summary("r04_pmc_v1.json", "c2", "cur")
+    summary("r04_pmc_v2.json", "c2", "old")      # newer, other sources
+    summary("r04_pmc_v3.json", "c2", None)       # no hash: historical
+    summary("r04_pmc_c3_v1.json", "c3", "cur")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "src_hash", lambda: "cur")
     _, src2 = bench.pmc_traffic(args("c2"))
     _, src3 = bench.pmc_traffic(args("c3"))
-    _, src4 = bench.pmc_traffic(args("c4"))
-    assert src2 and "_c3" not in src2 and "_c4" not in src2
-    assert src3 and "_c3" in src3
-    assert src4 and "_c4" in src4
+    assert src2 == os.path.join("profiles", "r04_pmc_v1.json")
+    assert src3 == os.path.join("profiles", "r04_pmc_c3_v1.json")
+    assert bench.pmc_traffic(args("c4")) == ({}, None)
     # same config, a batch no summary was collected on
     assert bench.pmc_traffic(args("c2", batch=3)) == ({}, None)
+
+
+def test_src_hash_ignores_comments():
+    sys.path.insert(0, ROOT)
+    import bench
+    h = bench.src_hash()
+    assert len(h) == 16 and h == bench.src_hash()
 
 
 def test_kernel_stats_files_sort_numerically():
@@ -106,10 +142,16 @@ def test_rocprof_kernel_match_is_whole_name(tmp_path, monkeypatch):
         '"Name","Calls","TotalDurationNs","AverageNs"\n'
         '"_ZN3sfm11k_score_mf2INS_9PackedSrcEEEvT_",2,10000000,5000000\n'
         '"_ZN3sfm10k_mf_candsEiPKi",2,20000,10000\n')
+    (prof / "r09_kernel_stats_v1.meta.json").write_text(json.dumps({"src_hash": "cur"}))
+    (prof / "r09_kernel_stats_v2.csv").write_text((prof / "r09_kernel_stats_v1.csv").read_text())
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "src_hash", lambda: "cur")
 
     class A:
         config = "c2"
+    # v2 has no .meta.json (recorded from unknown sources): only v1 counts
     ms, src = bench.rocprof_kernel_ms(A, ("k_score_mf2", "k_mf_cands"))
     assert abs(ms - 5.01) < 1e-9 and src.endswith("r09_kernel_stats_v1.csv")
     assert bench.rocprof_kernel_ms(A, ("k_score_mf", "k_mf_cands"))[0] is None
+    monkeypatch.setattr(bench, "src_hash", lambda: "new")
+    assert bench.rocprof_kernel_ms(A, ("k_score_mf2", "k_mf_cands")) == (None, None)

@@ -2,9 +2,12 @@
 configs[4], C5: LO-RANSAC 8192 hypotheses + local E refinement, fp32 vs fp16
 inlier-set parity sweep).
 
-* 32 / 16 evaluate ComputeError<float> / <half> (ransac5.hip:inlier_lowp):
-  bit-exact against the oracle's restatement (ransac5_oracle.cpp:is_inlier_lp),
-  itself checked against numpy float16/float32 arithmetic on the CPU.
+* 32 / 16 evaluate ComputeError<float> / <half> with E held in T
+  (ransac5.hip:inlier_lowp): bit-exact against the oracle's restatement
+  (ransac5_oracle.cpp:is_inlier_lp), itself checked against numpy
+  float16/float32 arithmetic on the CPU.
+* 33 / 17 are the literal template form (double Ematrix, double products,
+  sums rounded to T; ransac5.hip:inlier_lowp_tpl vs is_inlier_lp_tpl).
 * C5 at full size: one KITTI pair (N = 435,032), H = 8192, each precision's
   winner refined by the GPU IRLS (optimise); the agreement table of
   DESIGN.md §C5 is asserted here against its documented bounds."""
@@ -22,9 +25,11 @@ def _scene(seed, n=3000):
     return geometric_scene(np.random.default_rng(seed), n, out_frac=0.2, noise=0.002)
 
 
-@pytest.mark.parametrize("prec", [32, 16])
+@pytest.mark.parametrize("prec", [32, 16, 33, 17])
 @pytest.mark.parametrize("thr", [1e-3, 1e-2])
 def test_lowp_scoring_bit_exact_vs_oracle(cuda, prec, thr):
+    """32 / 16: E and every operation held in T; 33 / 17: the literal
+    ComputeError<T> with the reference's double Ematrix (is_inlier_lp_tpl)."""
     from sfm_amd import ransac
     q, qp = _scene(int(prec + 1e4 * thr))
     pts = torch.from_numpy(np.c_[q, qp]).unsqueeze(0).to(cuda)

@@ -224,3 +224,43 @@ def test_psnet_without_context_is_the_hot_path_chain(cuda):
                            out_hw=(128, 192))
     assert torch.equal(d_init, d)
     assert torch.equal(d, want)
+
+
+def test_psnet_predict_by_depth_init_is_unscaled(cuda):
+    """PREDICT_BY_DEPTH at MIN_DEPTH = 2: the reference returns depthregression's
+    output as depth_init and scales only depth by mindepth (PSNet.py:200-202 vs
+    209-210); with PSNET_CONTEXT off both come from the same cost, so
+    depth == 2 * depth_init exactly."""
+    from sfm_amd.config import defaults
+    from sfm_amd.psnet import PSNet
+    c = defaults()
+    c.update(PSNET_CONTEXT=False, PREDICT_BY_DEPTH=True, MIN_DEPTH=2.0)
+    torch.manual_seed(2)
+    net = PSNet(16, cfg=c).to(cuda).eval()
+    ref, tgt, K, pose = _psnet_inputs(cuda)
+    with torch.no_grad():
+        d_init, d = net(ref, [tgt], pose.unsqueeze(1).clone(), K, torch.inverse(K))
+    assert net.mindepth == 2.0
+    assert torch.equal(d_init * 2.0, d)
+
+
+def test_psnet_ind_context_feeds_dep_convs(cuda):
+    """IND_CONTEXT with PSNET_CONTEXT: the reference reassigns refimg_fea =
+    context_net(ref) (PSNet.py:177-178), so PSNET_DEP_CONTEXT upsamples the
+    context features, not feature_extraction's (PSNet.py:219)."""
+    import torch.nn.functional as F
+    from sfm_amd.config import defaults
+    from sfm_amd.psnet import PSNet
+    c = defaults()
+    c.update(PSNET_CONTEXT=True, IND_CONTEXT=True, PSNET_DEP_CONTEXT=True)
+    torch.manual_seed(3)
+    net = PSNet(16, 1.0, cfg=c).to(cuda).eval()
+    ref, tgt, K, pose = _psnet_inputs(cuda)
+    rec = {}
+    net.context_net.register_forward_hook(lambda m, i, o: rec.__setitem__("ctx", o.detach().clone()))
+    net.dep_convs.register_forward_pre_hook(lambda m, i: rec.__setitem__("dep_in", i[0].detach().clone()))
+    with torch.no_grad():
+        net(ref, [tgt], pose.unsqueeze(1).clone(), K, torch.inverse(K))
+        up = F.interpolate(rec["ctx"].float(), list(ref.shape[2:]), mode="bilinear", align_corners=True)
+    assert rec["dep_in"].shape[1] == 36
+    assert torch.equal(rec["dep_in"][:, 1:33], up)

@@ -158,3 +158,25 @@ def test_lowp_inlier_oracle_matches_numpy(prec):
             a = R.inlier_mask(E, q, qp, thr, prec)
             b = R.inlier_mask_numpy(E, q, qp, thr, prec)
             assert np.array_equal(a, b), (thr, int((a != b).sum()))
+
+
+@pytest.mark.parametrize("prec", [33, 17])
+def test_lowp_template_oracle_matches_numpy(prec):
+    """ransac5_oracle.cpp:is_inlier_lp_tpl -- the literal ComputeError<T> with the
+    reference's double Ematrix (kernel_functions.cu:231-264, common.h:26) -- vs
+    numpy's float64 products / float16|float32 roundings, on geometric and random
+    E of very different scales (no normalisation in this form: tiny E underflow
+    in half) and thresholds.  In half the two low-precision forms differ.""" 
+    from oracle.gen_golden import geometric_scene
+    rng = np.random.default_rng(prec)
+    q, qp = geometric_scene(rng, 4000, out_frac=0.3, noise=0.003)
+    r = R.ransac5(q, qp, iters=1, thr=1e-3, nchains=32)
+    Es = [r["E"], r["E"] * 1e-7, r["E"] * 3e6] + [rng.normal(size=(3, 3)) * s for s in (1e-9, 1.0, 1e3)]
+    differs = 0
+    for E in Es:
+        for thr in (1e-4, 1e-3, 1e-2, 0.5):
+            a = R.inlier_mask(E, q, qp, thr, prec)
+            b = R.inlier_mask_numpy_tpl(E, q, qp, thr, prec)
+            assert np.array_equal(a, b), (thr, int((a != b).sum()))
+            differs += int((a != R.inlier_mask(E, q, qp, thr, prec - 1)).sum())
+    assert prec == 33 or differs > 0

@@ -62,3 +62,17 @@ def test_missing_flow_estimator_is_named():
     m = SFMnet(128)
     with pytest.raises(RuntimeError, match="flow_estimator="):
         m._flow()
+
+
+def test_default_depth_precision_is_the_references():
+    """SFMnet(nlabel) regularises in fp32 (the reference's PSNet precision,
+    PSNet.py:159-165); bf16 is an explicit opt-in (VERDICT r03 Missing #2)."""
+    from models.SFMnet import SFMnet
+    from sfm_amd.config import kitti
+    from sfm_amd.psnet import PSNet
+    from sfm_amd.regularize import CostRegularization
+    import inspect
+    assert SFMnet(128).depth_estimator.conv_precision == "fp32"
+    assert SFMnet(128, cfg=kitti()).depth_estimator.conv_precision == "fp32"
+    assert inspect.signature(CostRegularization.forward).parameters["precision"].default == "fp32"
+    assert PSNet(16, 1.0, conv_precision="bf16").conv_precision == "bf16"
