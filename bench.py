@@ -87,6 +87,9 @@ def parse(argv=None):
                     help="each step's sweep on a side stream, overlapping the next step's pose stage "
                          "(TwoViewHotPath.step_pipelined): c2 +1.7 %%, sparse +12 %% pairs/s, but the overlapped "
                          "kernels' launch durations (the roofline fields) then include the overlap")
+    ap.add_argument("--overlap-ref", type=int, default=0, choices=(0, 1),
+                    help="1: the cost volume's pose-independent reference half on a side stream beside the RANSAC "
+                         "scorer (TwoViewHotPath.step_overlap); the sweep after RANSAC writes the warped half")
     args = ap.parse_args(argv)
     b, hw, it, nl, cd, kp = CONFIGS[args.config]
     args.batch = b if args.batch is None else args.batch
@@ -165,7 +168,7 @@ def rocprof_kernel_ms(args, prefixes):
     """Average launch duration (ms) of the kernels named by ``prefixes`` (summed:
     one launch each per step) from the newest committed rocprofv3 --stats
     summary of this workload (profiles/rNN_kernel_stats[_cfg]_vK.csv, written
-    by scripts/gpu_profile.sh from a profiled run of this bench), so the line
+    by scripts/gpu_evidence.sh from a profiled run of this bench), so the line
     carries a frac that follows from the committed profile, beside the live
     HIP-event one.  Only a summary recorded from these sources counts
     (its .meta.json sidecar's src_hash)."""
@@ -192,9 +195,9 @@ def rocprof_kernel_ms(args, prefixes):
     return (tot if hit == set(prefixes) else None), os.path.relpath(best[1], ROOT)
 
 
-ROOFLINE_REGIONS = ("ransac_score", "plane_sweep")
+ROOFLINE_REGIONS = ("ransac_score", "plane_sweep", "ref_planes")
 ALL_REGIONS = ("flow_to_points", "keypoints_to_points", "ransac_solve", "ransac_chain", "ransac_score",
-               "ransac_select", "plane_sweep")
+               "ransac_select", "plane_sweep", "ref_planes")
 
 
 def profiled_pass(stepf, inputs, steps, dev):
@@ -437,7 +440,8 @@ def _main_gpu(args, dist):
         kp = synth.keypoints(B, args.keypoints, hw, seed=rank, device=dev)
     hp = TwoViewHotPath(B, hw, fhw, C, args.nlabel, args.iters, args.threshold, 1.0, rescale_depth=True,
                         norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused,
-                        keypoints=None if kp is None else (kp, [args.keypoints] * B))
+                        keypoints=None if kp is None else (kp, [args.keypoints] * B),
+                        overlap_ref=bool(args.overlap_ref))
 
     # --pipeline: step i's sweep (side stream) overlaps step i+1's pose stage
     stepf = hp.step_pipelined if args.pipeline else hp.step
@@ -484,7 +488,13 @@ def _main_gpu(args, dist):
         2.0 ** -15 <= args.threshold < 1.0
     h, w = fhw
     s = 4 if cost_dtype == torch.float32 else 2
-    sweep_bytes = B * (2 * C * args.nlabel * h * w * s + 2 * C * h * w * 4)
+    if args.overlap_ref:
+        # the sweep kernel writes the warped half (and reads tgt); the reference
+        # half (writes + its padded ref reads) is k_ref_planes' on the side stream
+        sweep_bytes = B * (C * args.nlabel * h * w * s + C * h * w * 4)
+        ref_bytes = B * (C * args.nlabel * h * w * s + C * h * w * 4)
+    else:
+        sweep_bytes = B * (2 * C * args.nlabel * h * w * s + 2 * C * h * w * 4)
     sweep_gbs = sweep_bytes / (kt["plane_sweep"] * 1e-3) / 1e9
     hyps = B * 512 * args.iters
 
@@ -512,7 +522,8 @@ def _main_gpu(args, dist):
                                     f"nlabel={args.nlabel}, C=32 at {h}x{w}, {args.cost_dtype} cost volume"),
                        "pairs_per_gpu": B, "global_batch": world * B, "parallelism": f"dp{world}",
                        "streams": "sweep on a side stream (overlaps the next step's solve)" if args.pipeline
-                       else "one stream"},
+                       else ("reference half on a side stream beside the scorer" if args.overlap_ref
+                             else "one stream")},
             "dist": {"world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
                      "backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
                      "devices": names},
@@ -524,6 +535,14 @@ def _main_gpu(args, dist):
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,
                                "avg_launch_ms": round(kt["plane_sweep"], 4),
                                "bytes_per_launch": sweep_bytes},
+            "roofline_ref_planes": ({"kernel": "ref_planes (k_ref_pad + k_ref_planes, side stream beside the scorer)",
+                                     "bound": "hbm", "avg_launch_ms": round(kt["ref_planes"], 4),
+                                     "bytes_per_launch": ref_bytes,
+                                     "achieved": round(ref_bytes / (kt["ref_planes"] * 1e-3) / 1e9, 1),
+                                     "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                     "note": "runs concurrently with k_score_mf2: its duration includes sharing "
+                                             "the CUs with the scorer; not on the step's critical path"}
+                                    if args.overlap_ref and "ref_planes" in kt else None),
             "solve": {"hypotheses_per_launch": hyps, "ms": round(kt_all["ransac_solve"], 4),
                       "hypotheses_per_s": round(hyps / (kt_all["ransac_solve"] * 1e-3), 1)},
             "kernel_ms": {k: round(v, 4) for k, v in {**kt_all, **kt}.items()},

@@ -1925,6 +1925,13 @@ __global__ __launch_bounds__(64) void k_roots_split(int H, int lanes, double* __
 #endif
 }
 
+// Score fence (sfm_score_fence_enable / _wait): an event recorded on the
+// RANSAC stream right before the scoring phase, so that a second stream can
+// start pose-independent memory work (the cost volume's reference half) beside
+// the compute-bound scorer instead of beside the latency-bound solve.
+static hipEvent_t g_score_fence = nullptr;
+static bool g_score_fence_on = false;
+
 template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
@@ -2004,6 +2011,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     SFM_HIP(hipMemsetAsync(w.cov, 0, (size_t)bc * cmax * 8, s));
     SFM_HIP(hipMemsetAsync(w.best_lb, 0, SFM_MAX_BATCH * kBestStride * 4, s));
   }
+  if (g_score_fence_on && g_score_fence) SFM_HIP(hipEventRecord(g_score_fence, s));
   {
     ProfScope ps("ransac_score", s);
     score_dispatch(src, pp, bc, cmax, ScoreBufs{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim}, kc, mp, use_mf,
@@ -2128,6 +2136,18 @@ int sfm_ransac5_flow(const float* flow, int batch, int H, int W, int h_side, int
   const FlowSrc src{flow, Kinv, H, W, w_side - 2 * margin, margin, 1.0 / (double)(w_side - 2 * margin)};
   return run_src(src, n.data(), batch, num_test, num_ransac_test, iters, thr, seed, cheirality, workspace,
                  workspace_bytes, E_out, P_out, inliers_out, winner_out, hyp_score_out, (hipStream_t)stream);
+}
+
+int sfm_score_fence_enable(int on) {
+  if (on && !g_score_fence) SFM_HIP(hipEventCreateWithFlags(&g_score_fence, hipEventDisableTiming));
+  g_score_fence_on = on != 0;
+  return SFM_OK;
+}
+
+int sfm_score_fence_wait(void* stream) {
+  SFM_REQUIRE(g_score_fence, "score fence not enabled");
+  SFM_HIP(hipStreamWaitEvent((hipStream_t)stream, g_score_fence, 0));
+  return SFM_OK;
 }
 
 size_t sfm_score_essentials_workspace_bytes(int batch, int ncand) {

@@ -55,7 +55,7 @@
 // count can pass 63 spans x 1024 points), so the table fits beside the LDS
 // copy of the span's points.
 #ifndef SFM_MF2_TBL
-#define SFM_MF2_TBL 1
+#define SFM_MF2_TBL 2
 #endif
 // the float64 drain reads its points from global memory (L2) instead of an LDS
 // copy of the span: the 32 KB make room for the count table
@@ -64,6 +64,14 @@
 #endif
 #ifndef SFM_MF2_FOLD
 #define SFM_MF2_FOLD 1
+#endif
+// Experiment builds only (timing of the parts; WRONG counts): bit 1 skips the
+// undecided queue and float64 drain, bit 2 the count reduction and publishing
+// (the decision strings go to a sink instead), bit 4 the per-run A-row reloads
+// (every run reuses its first rows), bit 8 the span staging after a block's
+// first span (profiles/r04_mf2_parts_ab.txt).
+#ifndef SFM_MF2_EXP
+#define SFM_MF2_EXP 0
 #endif
 #ifndef SFM_MF2_BPRE
 #define SFM_MF2_BPRE 0
@@ -338,6 +346,10 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   uint32_t* queue = s_queue[wv];
   const _Float16* fr = &s_frag[0][0][0][0];
   constexpr int kTileHalves = 3 * 64 * 8;
+#if SFM_MF2_EXP
+  uint32_t exp_sink = 0u;
+  bool exp_first = true;
+#endif
   int b = 0;
 #if !SFM_MF2_DYN
   long long u = u_beg;
@@ -461,8 +473,14 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #if !SFM_MF2_GPTS
       s_pts[i] = v;
 #endif
+#if SFM_MF2_EXP & 8
+      if (exp_first)
+#endif
       mf_stage_point(v, live, &s_frag[i >> 5][0][0][0], i & 31);
     }
+#if SFM_MF2_EXP & 8
+    exp_first = false;
+#endif
     MF_STAMP(0);
     lds_barrier();
     MF_STAMP(5);
@@ -598,11 +616,14 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #else
       const int kn = claim();
 #endif
-      if (kn < k1) load_rows(b, kn, ctot);
+      if (!(SFM_MF2_EXP & 4) && kn < k1) load_rows(b, kn, ctot);
       MF_STAMP(6);
       // 3. undecided evaluations -> the queue -> float64.  Bit j of a string
       // is tile kMf2Tiles-1-j, point 32 (kMf2Tiles-1-j) + rl of the span.
       int nl = 0;
+#if SFM_MF2_EXP & 1
+      if (false)
+#endif
 #pragma unroll
       for (int g = 0; g < 16; ++g) nl += __popc(mf2_undecided(s1[g], s2[g]));
       const int incl = mf_wave_scan(nl, lane);
@@ -678,6 +699,11 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       }
       MF_STAMP(2);
       // 4. counts: popcounts of the inlier strings over the 32 points of each half + the float64 counts
+#if SFM_MF2_EXP & 2
+#pragma unroll
+      for (int g = 0; g < 16; ++g) exp_sink ^= s1[g] ^ s2[g];
+      if (false) {
+#endif
       int cT[16];
 #pragma unroll
       for (int g = 0; g < 16; ++g) cT[g] = __popc(s1[g]);
@@ -698,6 +724,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
             atomicAdd(cntT + (size_t)b * cmax + c0 + c, d);
         }
       }
+#if SFM_MF2_EXP & 2
+      }
+#endif
       wave_sync();
       MF_STAMP(4);
       k = kn;
@@ -713,6 +742,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   // (DYN: the loop left right after a block barrier; static ranges: after the
   // last span's barrier)
   if (tb >= 0) flush(tb);
+#endif
+#if SFM_MF2_EXP
+  if (exp_sink == 0x9e3779b9u) cntT[0] = 1;                 // keeps the sinked strings live
 #endif
 #if SFM_MF2_DYN
   // the last block out zeroes the counters (claim[8] counts finished blocks),

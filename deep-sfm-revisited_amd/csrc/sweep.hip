@@ -383,6 +383,8 @@ struct FlatGeom {
   int buf_ok;      // k_sweep_tile fast path: per-pair volume, ref and quad ranges < 2^32 bytes, pair_ok
   int share;       // k_sweep_tile fast path: neighbour-lane tap sharing (tuning key sweep_share)
   int store_nt;    // k_sweep_tile fast path: non-temporal volume stores (tuning key sweep_store_nt)
+  int write_ref;   // k_sweep_tile: write the reference rows too (0: the warped half only, the reference
+                   // half comes from k_ref_planes, e.g. on a side stream beside RANSAC)
   unsigned pair_bytes;   // one pair's output volume in bytes (buffer range)
   Magic mwin, mgrp, mhw;
   float inv_w;
@@ -653,7 +655,7 @@ __device__ __forceinline__ void sweep_tile_item(const float* __restrict__ ref, c
   }
   const int nc = min(G, g.C - c0);
   float cp[G][NJ];
-  if (g.ref_rows) {
+  if (g.ref_rows && g.write_ref) {
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       if (c >= nc) break;
@@ -735,7 +737,7 @@ __device__ __forceinline__ void sweep_tile_item(const float* __restrict__ ref, c
       }
     }
   };
-  if (g.ref_rows) {
+  if (g.ref_rows && g.write_ref) {
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       if (c >= nc) break;
@@ -796,7 +798,7 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
   const __amdgpu_buffer_rsrc_t rout = buf_rsrc(out + (size_t)b * g.rows * g.slab, g.pair_bytes);
   const unsigned row_bytes = (unsigned)g.slab * (unsigned)sizeof(OutT);
   float cp[G][NJ];
-  if (g.ref_rows) {
+  if (g.ref_rows && g.write_ref) {
     const __amdgpu_buffer_rsrc_t rref = buf_rsrc(ref + ((size_t)b * g.C + c0) * g.hw, (unsigned)G * g.hw * 4u);
 #pragma unroll
     for (int c = 0; c < G; ++c)
@@ -940,7 +942,7 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       }
     }
   };
-  if (g.ref_rows) {
+  if (g.ref_rows && g.write_ref) {
 #pragma unroll
     for (int c = 0; c < G; ++c) store_row((unsigned)(c0 + c), cp[c]);
   }
@@ -1338,7 +1340,7 @@ static size_t sweep_ws_bytes(int B, int C, int h, int w) { return sweep_core_byt
 static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B, int C, int h, int w,
                         const float* pose, const float* K4, const float* K4inv, int L, float min_depth,
                         int depth_mode, int out_dtype, void* out, void* ws, size_t ws_bytes, hipStream_t s,
-                        const PsnetPrep& prep = PsnetPrep{}) {
+                        const PsnetPrep& prep = PsnetPrep{}, bool write_ref = true) {
   SFM_REQUIRE(tgt && pose && K4 && K4inv && out && (!with_ref || ref), "null pointer argument");
   SFM_REQUIRE(B >= 1 && B <= 65535 && C >= 1 && C <= 4 * 65535 && h >= 2 && w >= 2 && L >= 1,
               "invalid sweep shape");   // k_tgt_quads' grid: quads in y, pairs in z
@@ -1445,6 +1447,7 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     fg.buf_ok = pair_bytes < ((int64_t)1 << 32) && (out_dtype == 0 || fg.pair_ok) && tuning().sweep_buffer;
     fg.share = tuning().sweep_share;
     fg.store_nt = tuning().sweep_store_nt == 2 ? out_dtype != 0 : tuning().sweep_store_nt;   // auto: bf16 only
+    fg.write_ref = write_ref ? 1 : 0;
     fg.pair_bytes = fg.buf_ok ? (unsigned)pair_bytes : 0u;
     fg.mwin = make_magic((unsigned)nwin);
     fg.mgrp = make_magic((unsigned)fgroups);
@@ -1477,6 +1480,125 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   }
   SFM_LAUNCHED();
   return SFM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// The volume's reference half on its own (round 4).  cost[b][c][l] =
+// ref[b][c] for every plane l (PSNet.py:155) does not depend on the pose, so
+// the hot path writes it on a side stream while RANSAC runs and the sweep
+// after RANSAC writes only the warped half (k_sweep_tile with write_ref = 0).
+// The scorer is compute-bound and leaves the memory system idle, but it holds
+// 3 waves x 168 VGPRs per SIMD: k_ref_planes is built to fit the remaining 8
+// VGPRs (one wave per SIMD beside the scorer's three).
+//   k_ref_pad:    ref [B*C][hw] -> rp [B*C][hw + kRefPad], rp[i] = ref[i mod hw]
+//                 (a row and its first kRefPad elements again, so that six
+//                 consecutive 64-element chunks never wrap)
+//   k_ref_planes: persistent; wave w copies the w-th contiguous range of the
+//                 64-element chunks of every pair's reference half (C slabs of
+//                 L * hw elements, chunks never straddle a slab: L * hw % 64
+//                 == 0); lane i of a chunk at slab element e reads rp[c][e mod
+//                 hw] (one dword, L2-resident) and writes it, so a wave store
+//                 is one aligned 256-byte segment.  Six chunks per iteration.
+// Same values as the full sweep's reference rows (a copy; bf16 by the same
+// RNE conversion).  Shapes outside the fast path take k_ref_planes_generic.
+// ---------------------------------------------------------------------------
+constexpr int kRefUnroll = 4;   // dwords in flight per lane: 8 VGPRs in all
+constexpr int kRefPad = 64 * kRefUnroll;
+
+__global__ __launch_bounds__(256) void k_ref_pad(const float* __restrict__ ref, int hw, float* __restrict__ rp) {
+  const size_t row = blockIdx.y;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < hw + kRefPad; i += gridDim.x * 256)
+    rp[row * (size_t)(hw + kRefPad) + i] = ref[row * (size_t)hw + (i < hw ? i : (i - hw) % hw)];
+}
+
+template <typename OutT>
+__device__ __forceinline__ void ref_bstore(__amdgpu_buffer_rsrc_t r, float v, unsigned voff, unsigned soff);
+template <>
+__device__ __forceinline__ void ref_bstore<float>(__amdgpu_buffer_rsrc_t r, float v, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff * 4u, soff * 4u, 0);
+}
+template <>
+__device__ __forceinline__ void ref_bstore<unsigned short>(__amdgpu_buffer_rsrc_t r, float v, unsigned voff,
+                                                           unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b16(to_bf16(v), r, voff * 2u, soff * 2u, 0);
+}
+template <typename OutT>
+__device__ __forceinline__ void ref_store(OutT* dst, float v);
+template <>
+__device__ __forceinline__ void ref_store<float>(float* dst, float v) { *dst = v; }
+template <>
+__device__ __forceinline__ void ref_store<unsigned short>(unsigned short* dst, float v) { *dst = to_bf16(v); }
+
+// One wave's share of the chunks, and the uniform decode constants (host-made:
+// no integer division on the device, whose VALU expansion would hold VGPRs).
+struct RefPlanes {
+  unsigned cps;        // 64-element chunks per slab (L * hw / 64)
+  unsigned q, r;       // total chunks / waves, remainder: wave w takes q (+1 if w < r)
+  int C, hw, L;
+  Magic mcps, mC, mhw;
+};
+
+// grid: one 256-thread block per CU (one wave per SIMD).  Buffer addressing
+// keeps the per-lane state to the source offset and the lane's element: every
+// uniform part of an address is an SGPR (resource base, soffset).
+template <typename OutT>
+__global__ __launch_bounds__(256) void k_ref_planes(const float* __restrict__ rp, RefPlanes g,
+                                                    OutT* __restrict__ out) {
+  const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const unsigned w = blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  unsigned m = w * g.q + min(w, g.r);
+  const unsigned hi = m + g.q + (w < g.r ? 1u : 0u);
+  const unsigned slab_bytes = (unsigned)g.L * (unsigned)g.hw * (unsigned)sizeof(OutT);
+  const unsigned hw = (unsigned)g.hw;
+  while (m < hi) {
+    // uniform: slab (pair b, channel c) and chunk j of m
+    const unsigned sl = magic_div(m, g.mcps);
+    const unsigned j = m - sl * g.cps;
+    const unsigned b = magic_div(sl, g.mC), c = sl - b * (unsigned)g.C;
+    unsigned n = min(hi - m, g.cps - j);
+    const __amdgpu_buffer_rsrc_t rsrc = buf_rsrc(rp + ((size_t)b * g.C + c) * (size_t)(hw + kRefPad),
+                                                 (hw + kRefPad) * 4u);
+    const __amdgpu_buffer_rsrc_t rdst = buf_rsrc(out + ((size_t)b * 2 * g.C + c) * (size_t)g.L * hw, slab_bytes);
+    unsigned e = j * 64u;                                      // slab element of the chunk (uniform)
+    const unsigned e0 = e - magic_div(e, g.mhw) * hw;          // e mod hw
+    unsigned p = e0 + lane;                                    // source element of this lane
+    p = min(p, p - hw);                                        // mod hw (unsigned wrap: the smaller is it)
+    m += n;
+    for (; n >= (unsigned)kRefUnroll; n -= kRefUnroll) {
+      float v[kRefUnroll];
+#pragma unroll
+      for (int k = 0; k < kRefUnroll; ++k)
+        v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, p * 4u, 256u * k, 0));
+#pragma unroll
+      for (int k = 0; k < kRefUnroll; ++k) ref_bstore<OutT>(rdst, v[k], lane, e + 64u * k);
+      e += 64u * kRefUnroll;
+      p += 64u * kRefUnroll;
+      p = min(p, p - hw);
+    }
+    for (; n > 0; --n) {
+      ref_bstore<OutT>(rdst, __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, p * 4u, 0u, 0)), lane, e);
+      e += 64u;
+      p += 64u;
+      p = min(p, p - hw);
+    }
+  }
+}
+
+// any shape: one thread per element of the reference half
+template <typename OutT>
+__global__ __launch_bounds__(256) void k_ref_planes_generic(const float* __restrict__ ref, int C, int hw, int L,
+                                                            OutT* __restrict__ out) {
+  const size_t slab = (size_t)L * hw;
+  const size_t bc = blockIdx.y;                              // b * C + c
+  const size_t b = bc / C, c = bc - b * C;
+  OutT* dst = out + (b * 2 * C + c) * slab;
+  const float* src = ref + bc * hw;
+  for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < slab; e += (size_t)gridDim.x * 256)
+    ref_store<OutT>(dst + e, src[e % hw]);
+}
+
+static size_t ref_planes_ws_bytes(int B, int C, int h, int w) {
+  return (((size_t)B * C * ((size_t)h * w + kRefPad) * sizeof(float)) + 255) & ~(size_t)255;
 }
 
 }  // namespace sfm
@@ -1533,6 +1655,89 @@ int sfm_plane_sweep_psnet(const float* ref, const float* tgt, int batch, int cha
                       prep + (size_t)batch * 21, nlabel, min_depth, depth_mode, out_dtype, cost, workspace,
                       sweep_core_bytes(batch, channels, h, w), s,
                       PsnetPrep{pose, pose_dtype, K, Kinv, t_scale, prep});
+}
+
+size_t sfm_plane_sweep_ref_planes_workspace_bytes(int batch, int channels, int h, int w) {
+  if (batch < 1 || channels < 1 || h < 1 || w < 1) return 0;
+  return ref_planes_ws_bytes(batch, channels, h, w);
+}
+
+int sfm_plane_sweep_ref_planes(const float* ref, int batch, int channels, int h, int w, int nlabel, int out_dtype,
+                               void* cost, void* workspace, size_t workspace_bytes, void* stream) {
+  SFM_REQUIRE(ref && cost, "null pointer argument");
+  SFM_REQUIRE(batch >= 1 && batch <= 65535 && channels >= 1 && channels <= 65535 && h >= 1 && w >= 1 && nlabel >= 1,
+              "invalid sweep shape");
+  SFM_REQUIRE(out_dtype == 0 || out_dtype == 1, "out_dtype must be 0 (float32) or 1 (bfloat16)");
+  SFM_REQUIRE((int64_t)h * w < ((int64_t)1 << 30), "feature map too large");
+  hipStream_t s = (hipStream_t)stream;
+  const int hw = h * w;
+  const int64_t slab = (int64_t)nlabel * hw;
+  const int esz = out_dtype == 0 ? 4 : 2;
+  // fast path: chunks within slabs, a padded row that six chunks never wrap, 256-byte aligned slabs
+  // (magic_div needs n < 2^31: chunk counts and slab elements)
+  const bool fast = slab % 64 == 0 && hw >= kRefPad && ((uintptr_t)cost % 256) == 0 && (slab * esz) % 256 == 0 &&
+                    (int64_t)batch * channels * (slab / 64) < ((int64_t)1 << 31) && slab < ((int64_t)1 << 31) &&
+                    slab * esz < ((int64_t)1 << 32) && workspace &&
+                    workspace_bytes >= ref_planes_ws_bytes(batch, channels, h, w);
+  ProfScope ps("ref_planes", s);
+  if (fast) {
+    float* rp = (float*)workspace;
+    hipLaunchKernelGGL(k_ref_pad, dim3((hw + kRefPad + 255) / 256, (unsigned)(batch * channels)), dim3(256), 0, s,
+                       ref, hw, rp);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    cus = std::max(1, cus);
+    RefPlanes g;
+    g.cps = (unsigned)(slab / 64);
+    const unsigned waves = (unsigned)cus * 4u;
+    const int64_t total = (int64_t)batch * channels * g.cps;
+    g.q = (unsigned)(total / waves);
+    g.r = (unsigned)(total % waves);
+    g.C = channels; g.hw = hw; g.L = nlabel;
+    g.mcps = make_magic(g.cps); g.mC = make_magic((unsigned)channels); g.mhw = make_magic((unsigned)hw);
+    if (out_dtype == 0)
+      hipLaunchKernelGGL(k_ref_planes<float>, dim3(cus), dim3(256), 0, s, rp, g, (float*)cost);
+    else
+      hipLaunchKernelGGL(k_ref_planes<unsigned short>, dim3(cus), dim3(256), 0, s, rp, g, (unsigned short*)cost);
+  } else {
+    const unsigned gx = (unsigned)std::min<int64_t>((slab + 255) / 256, 4096);
+    if (out_dtype == 0)
+      hipLaunchKernelGGL(k_ref_planes_generic<float>, dim3(gx, (unsigned)(batch * channels)), dim3(256), 0, s, ref,
+                         channels, hw, nlabel, (float*)cost);
+    else
+      hipLaunchKernelGGL(k_ref_planes_generic<unsigned short>, dim3(gx, (unsigned)(batch * channels)), dim3(256), 0,
+                         s, ref, channels, hw, nlabel, (unsigned short*)cost);
+  }
+  SFM_LAUNCHED();
+  return SFM_OK;
+}
+
+int sfm_plane_sweep_psnet_warped_half(const float* ref, const float* tgt, int batch, int channels, int h, int w, const void* pose,
+                                      int pose_dtype, const float* K, const float* Kinv, float t_scale, int nlabel,
+                                      float min_depth, int depth_mode, int out_dtype, void* cost, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  SFM_REQUIRE(ref && tgt && pose && K && Kinv && cost && workspace, "null pointer argument");
+  SFM_REQUIRE(batch >= 1 && channels >= 1 && h >= 2 && w >= 2, "invalid sweep shape");
+  SFM_REQUIRE(pose_dtype == 0 || pose_dtype == 1, "pose_dtype must be 0 (float32) or 1 (float64)");
+  SFM_REQUIRE(nlabel >= 1, "invalid sweep shape");
+  SFM_REQUIRE(out_dtype == 0 || out_dtype == 1, "out_dtype must be 0 (float32) or 1 (bfloat16)");
+  SFM_REQUIRE(depth_mode == 0 || depth_mode == 1, "depth_mode must be 0 (inverse depth) or 1 (depth)");
+  SFM_REQUIRE(min_depth > 0.0f, "min_depth must be positive");
+  SFM_REQUIRE((int64_t)h * w < ((int64_t)1 << 30), "feature map too large");
+  const size_t need = sweep_ws_bytes(batch, channels, h, w);
+  if (workspace_bytes < need) {
+    set_error("plane sweep workspace too small: need " + std::to_string(need) + " bytes");
+    return SFM_ERR_WORKSPACE;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  float* prep = reinterpret_cast<float*>((char*)workspace + sweep_core_bytes(batch, channels, h, w));
+  // the full volume's geometry (2C rows per plane) with its reference rows
+  // left to sfm_plane_sweep_ref_planes; windows off k_sweep_tile's fast path
+  // (edges, other sweep modes) still write them from `ref`: the same values
+  return launch_sweep(true, ref, tgt, batch, channels, h, w, prep, prep + (size_t)batch * 12,
+                      prep + (size_t)batch * 21, nlabel, min_depth, depth_mode, out_dtype, cost, workspace,
+                      sweep_core_bytes(batch, channels, h, w), s,
+                      PsnetPrep{pose, pose_dtype, K, Kinv, t_scale, prep}, false);
 }
 
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w, const float* pose,

@@ -38,7 +38,7 @@ def kinv3x3(K):
 class TwoViewHotPath:
     def __init__(self, batch, image_hw, feat_hw, channels=32, nlabel=128, iters=8, threshold=1e-4,
                  min_depth=1.0, rescale_depth=False, norm_target=0.6, cost_dtype=torch.float32, margin=10,
-                 device="cuda", seed=ransac.DEFAULT_SEED, fused=False, keypoints=None):
+                 device="cuda", seed=ransac.DEFAULT_SEED, fused=False, keypoints=None, overlap_ref=False):
         self.batch = int(batch)
         self.H, self.W = image_hw
         self.h, self.w = feat_hw
@@ -68,6 +68,13 @@ class TwoViewHotPath:
         self.cost = torch.empty(B, 2 * self.C, self.L, self.h, self.w, dtype=cost_dtype, device=self.device)
         self.cost_dtype = cost_dtype
         self.sweep_ws = sweep.workspace_for(B, self.C, self.h, self.w, self.device)
+        # overlap_ref: the volume's pose-independent reference half on a side
+        # stream beside the scorer (see step_overlap)
+        self.overlap_ref = bool(overlap_ref)
+        if self.overlap_ref:
+            self.ref_ws = sweep.ref_planes_workspace_for(B, self.C, self.h, self.w, self.device)
+            self.ref_stream = torch.cuda.Stream(device=self.device)
+            _lib.check(_lib.load().sfm_score_fence_enable(1), "sfm_score_fence_enable")
 
     @staticmethod
     def k_inverse(K):
@@ -121,7 +128,30 @@ class TwoViewHotPath:
             cost = self.sweep(ref_fea, tgt_fea, P, K, Kinv)
         return E, P, inl, cost
 
+    def step_overlap(self, flow, K, ref_fea, tgt_fea):
+        """``step`` with the cost volume's reference half (cost[:, :C, i] =
+        ref, PSNet.py:155: no pose needed) written on a side stream that waits
+        for the score fence, i.e. runs beside the compute-bound RANSAC scorer,
+        which leaves HBM idle; the sweep after RANSAC then writes only the
+        warped half.  The same volume bit for bit; the step returns after
+        both halves (the caller's stream waits for the side stream)."""
+        main = torch.cuda.current_stream(self.device)
+        side = self.ref_stream
+        side.wait_stream(main)                 # the previous step is done with the cost buffer
+        Kinv = self.k_inverse(K)
+        E, P, inl, win = self.pose(flow, K, Kinv)
+        with torch.cuda.stream(side):
+            _lib.check(_lib.load().sfm_score_fence_wait(_lib.stream_ptr(self.device)), "sfm_score_fence_wait")
+            sweep.plane_sweep_ref_half(ref_fea, self.L, self.cost, self.ref_ws)
+        ref_fea.record_stream(side)
+        cost = sweep.plane_sweep_cost_psnet(ref_fea, tgt_fea, P, K, Kinv, self.L, self.min_depth, self.rescale,
+                                            self.cost_dtype, out=self.cost, workspace=self.sweep_ws, warped_half=True)
+        main.wait_stream(side)
+        return E, P, inl, cost
+
     def step(self, flow, K, ref_fea, tgt_fea):
+        if self.overlap_ref:
+            return self.step_overlap(flow, K, ref_fea, tgt_fea)
         Kinv = self.k_inverse(K)
         E, P, inl, win = self.pose(flow, K, Kinv)
         cost = self.sweep(ref_fea, tgt_fea, P, K, Kinv)

@@ -84,15 +84,43 @@ def plane_sweep_cost(ref_fea, tgt_fea, pose, intrinsics4, intrinsics_inv4, nlabe
     return out
 
 
+def ref_planes_workspace_for(B, C, h, w, device):
+    n = _lib.load().sfm_plane_sweep_ref_planes_workspace_bytes(B, C, h, w)
+    return torch.empty(n, dtype=torch.uint8, device=device)
+
+
+def plane_sweep_ref_half(ref_fea, nlabel, out, workspace=None):
+    """The pose-independent reference half of the cost volume, cost[:, :C, i] =
+    ref for every plane (PSNet.py:155), into ``out`` [B, 2C, L, h, w]
+    (sfm_plane_sweep_ref_planes; typically on a side stream beside RANSAC)."""
+    ref = _dev_f32(ref_fea, "ref_fea")
+    B, C, h, w = ref.shape
+    if tuple(out.shape) != (B, 2 * C, int(nlabel), h, w) or not out.is_contiguous() or \
+            out.dtype not in (torch.float32, torch.bfloat16) or out.device != ref.device:
+        raise RuntimeError(f"out must be a contiguous float32/bfloat16 tensor of shape {(B, 2 * C, int(nlabel), h, w)}")
+    if workspace is None:
+        workspace = ref_planes_workspace_for(B, C, h, w, ref.device)
+    with torch.cuda.device(ref.device):
+        rc = _lib.load().sfm_plane_sweep_ref_planes(_lib.ptr(ref), B, C, h, w, int(nlabel),
+                                                    0 if out.dtype == torch.float32 else 1, _lib.ptr(out),
+                                                    _lib.ptr(workspace), workspace.numel(),
+                                                    _lib.stream_ptr(ref.device))
+        _lib.check(rc, "sfm_plane_sweep_ref_planes")
+    return out
+
+
 def plane_sweep_cost_psnet(ref_fea, tgt_fea, pose, intrinsics, intrinsics_inv, nlabel, min_depth=1.0,
-                           rescale=None, dtype=torch.float32, out=None, workspace=None, predict_by_depth=False):
+                           rescale=None, dtype=torch.float32, out=None, workspace=None, predict_by_depth=False,
+                           warped_half=False):
     """``plane_sweep_cost`` from the pose stage's outputs: ``pose`` [B,3,4]
     float32 or float64 (unscaled), full-resolution ``intrinsics`` /
     ``intrinsics_inv`` [B,3,3].  PSNet.forward's preparation (P.float(),
     RESCALE_DEPTH translation * ``rescale``, K/4 rows 0-1, K^-1[:2,:2]*4;
     PSNet.py:130-133) runs inside the call (sfm_plane_sweep_psnet), with the
     same float32 bits as ``quarter_intrinsics`` + ``plane_sweep_cost``.  Unlike
-    PlaneSweep it does not rescale the caller's pose in place."""
+    PlaneSweep it does not rescale the caller's pose in place.  ``warped_half``:
+    leave the reference rows to ``plane_sweep_ref_half``
+    (sfm_plane_sweep_psnet_warped_half)."""
     _refuse_grad(ref_fea=ref_fea, tgt_fea=tgt_fea, pose=pose, intrinsics=intrinsics, intrinsics_inv=intrinsics_inv)
     tgt = _dev_f32(tgt_fea, "tgt_fea")
     B, C, h, w = tgt.shape
@@ -116,14 +144,15 @@ def plane_sweep_cost_psnet(ref_fea, tgt_fea, pose, intrinsics, intrinsics_inv, n
     L = _lib.load()
     if workspace is None:
         workspace = workspace_for(B, C, h, w, tgt.device)
+    fn = L.sfm_plane_sweep_psnet_warped_half if warped_half else L.sfm_plane_sweep_psnet
     with torch.cuda.device(tgt.device):
-        rc = L.sfm_plane_sweep_psnet(_lib.ptr(ref), _lib.ptr(tgt), B, C, h, w, _lib.ptr(P),
+        rc = fn(_lib.ptr(ref), _lib.ptr(tgt), B, C, h, w, _lib.ptr(P),
                                      1 if P.dtype == torch.float64 else 0, _lib.ptr(K), _lib.ptr(Ki),
                                      float(rescale) if rescale is not None else 0.0, int(nlabel), float(min_depth),
                                      1 if predict_by_depth else 0, 0 if dtype == torch.float32 else 1,
                                      _lib.ptr(out), _lib.ptr(workspace), workspace.numel(),
                                      _lib.stream_ptr(tgt.device))
-        _lib.check(rc, "sfm_plane_sweep_psnet")
+        _lib.check(rc, "sfm_plane_sweep_psnet_warped_half" if warped_half else "sfm_plane_sweep_psnet")
     return out
 
 

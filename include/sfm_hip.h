@@ -243,6 +243,33 @@ int sfm_plane_sweep_psnet(const float* ref, const float* tgt, int batch, int cha
                           int nlabel, float min_depth, int depth_mode, int out_dtype, void* cost,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* The two halves of sfm_plane_sweep_psnet's volume separately, so that the
+ * pose-independent reference half (cost[:, :C, i] = ref, PSNet.py:155) can be
+ * written on a second stream while RANSAC runs (round 4; the scorer is
+ * compute-bound and leaves HBM idle):
+ *   sfm_plane_sweep_ref_planes         rows 0..C-1 of every pair's
+ *       [2C, nlabel, h, w] volume: a copy of ref per plane (bf16: RNE), in one
+ *       wave per SIMD with 8 VGPRs, which fits beside the scorer's waves.
+ *       workspace: sfm_plane_sweep_ref_planes_workspace_bytes (a padded copy
+ *       of ref); shapes off its fast path use a generic kernel.
+ *   sfm_plane_sweep_psnet_warped_half  sfm_plane_sweep_psnet without those rows
+ *       (windows off the sweep's fast path still write them from ref: the
+ *       same values).
+ * Together they write exactly sfm_plane_sweep_psnet's volume. */
+size_t sfm_plane_sweep_ref_planes_workspace_bytes(int batch, int channels, int h, int w);
+/* Score fence: with it enabled, every RANSAC call records a library-owned
+ * event on its stream right before its scoring phase; sfm_score_fence_wait
+ * makes `stream` wait for the last one recorded (so the reference half can run
+ * beside the compute-bound scorer rather than the latency-bound solve). */
+int sfm_score_fence_enable(int on);
+int sfm_score_fence_wait(void* stream);
+int sfm_plane_sweep_ref_planes(const float* ref, int batch, int channels, int h, int w, int nlabel, int out_dtype,
+                               void* cost, void* workspace, size_t workspace_bytes, void* stream);
+int sfm_plane_sweep_psnet_warped_half(const float* ref, const float* tgt, int batch, int channels, int h, int w,
+                                      const void* pose, int pose_dtype, const float* K, const float* Kinv,
+                                      float t_scale, int nlabel, float min_depth, int depth_mode, int out_dtype,
+                                      void* cost, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Warped half only (cost[b, c, i] = inverse_warp(tgt, d_i)), batch x C x nlabel x h x w. */
 int sfm_plane_sweep_warped(const float* tgt, int batch, int channels, int h, int w,
                            const float* pose, const float* K4, const float* K4inv,

@@ -92,14 +92,22 @@ def main(src, dst, config="c2"):
     json.dump({"source": "rocprofv3 --pmc --kernel-trace, separate passes (scripts/gpu_pmc.sh) over "
                          f"`python3 bench.py --config {config} --steps 1 --warmup 1 --no-cpu-baseline`",
                "workload": {"config": config, "batch": b, "nlabel": nl, "iters": it, "cost_dtype": cd},
-               "src_hash": _src_hash(),
+               "src_hash": _src_hash(src),
                "kernels": out}, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps({k: {x: v.get(x) for x in ("hbm_read_bytes", "hbm_write_bytes", "l2_hit_rate")}
                       for k, v in out.items()}, indent=1))
 
 
-def _src_hash():
-    """bench.src_hash() of the sources in this tree (the ones the counters were recorded from)."""
+def _src_hash(src=None):
+    """The src_hash of the profiled bench run (its JSON line in the pass logs
+    of gpu_pmc.sh), else bench.src_hash() of the sources in this tree."""
+    for log in sorted(glob.glob(os.path.join(src or "", "p*.log"))) if src else []:
+        for line in open(log, errors="replace"):
+            if line.startswith("{") and '"src_hash"' in line:
+                try:
+                    return json.loads(line)["src_hash"]
+                except ValueError:
+                    pass
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     return bench.src_hash()

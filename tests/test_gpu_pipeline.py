@@ -26,3 +26,42 @@ def test_pipelined_steps_equal_plain_steps(cuda):
         assert torch.equal(E, o[0]) and torch.equal(P, o[1]) and torch.equal(inl, o[2])
     torch.cuda.synchronize()
     assert torch.equal(plain.cost, piped.cost)            # the last step's volume
+
+
+@pytest.mark.parametrize("dtype,fhw,L", [(torch.float32, (94, 311), 32), (torch.bfloat16, (94, 311), 16),
+                                          (torch.float32, (20, 30), 8), (torch.float32, (12, 17), 5)])
+def test_overlapped_reference_half_equals_full_sweep(cuda, dtype, fhw, L):
+    """step_overlap: the reference half from sfm_plane_sweep_ref_planes on a
+    side stream behind the score fence, the warped half from
+    sfm_plane_sweep_psnet_warped_half.  Steps back to back; the volume must
+    equal the one-launch sweep's bit for bit, at KITTI size (fast copy path)
+    and at small / odd shapes (generic path: hw < the padding, L * hw % 64 != 0)."""
+    from sfm_amd import synth
+    from sfm_amd.pipeline import TwoViewHotPath
+    B, C = 2, 32
+    steps = []
+    for s in (21, 22):
+        flow, K, _, _ = synth.kitti_pair_batch(B, seed=s, device=cuda)
+        ref, tgt = synth.features(B, C, *fhw, seed=s, device=cuda)
+        steps.append((flow, K, ref, tgt))
+    mk = lambda ov: TwoViewHotPath(B, (376, 1242), fhw, C, L, 2, 1e-4, 1.0, True, 0.6, cost_dtype=dtype,
+                                   device=cuda, overlap_ref=ov)
+    plain, over = mk(False), mk(True)
+    for a in steps:
+        over.cost.fill_(float("nan"))                       # every element must be written this step
+        E2, P2, i2, c2 = over.step(*a)
+        E1, P1, i1, c1 = plain.step(*a)
+        torch.cuda.synchronize()
+        assert torch.equal(E1, E2) and torch.equal(P1, P2) and torch.equal(i1, i2)
+        assert torch.equal(c1, c2)
+
+
+def test_ref_planes_alone_write_only_the_reference_rows(cuda):
+    from sfm_amd import sweep, synth
+    B, C, L, h, w = 3, 32, 16, 94, 311
+    ref, _ = synth.features(B, C, h, w, seed=5, device=cuda)
+    out = torch.full((B, 2 * C, L, h, w), 7.0, device=cuda)
+    sweep.plane_sweep_ref_half(ref, L, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :C], ref.unsqueeze(2).expand(B, C, L, h, w))
+    assert bool((out[:, C:] == 7.0).all())
