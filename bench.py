@@ -87,9 +87,10 @@ def parse(argv=None):
                     help="each step's sweep on a side stream, overlapping the next step's pose stage "
                          "(TwoViewHotPath.step_pipelined): c2 +1.7 %%, sparse +12 %% pairs/s, but the overlapped "
                          "kernels' launch durations (the roofline fields) then include the overlap")
-    ap.add_argument("--overlap-ref", type=int, default=0, choices=(0, 1),
-                    help="1: the cost volume's pose-independent reference half on a side stream beside the RANSAC "
-                         "scorer (TwoViewHotPath.step_overlap); the sweep after RANSAC writes the warped half")
+    ap.add_argument("--overlap-ref", default="0", choices=("0", "score", "step"),
+                    help="the cost volume's pose-independent reference half on a side stream "
+                         "(TwoViewHotPath.step_overlap): 'score' beside the RANSAC scorer (behind the score fence), "
+                         "'step' from the start of the step; the sweep after RANSAC then writes the warped half")
     args = ap.parse_args(argv)
     b, hw, it, nl, cd, kp = CONFIGS[args.config]
     args.batch = b if args.batch is None else args.batch
@@ -441,7 +442,7 @@ def _main_gpu(args, dist):
     hp = TwoViewHotPath(B, hw, fhw, C, args.nlabel, args.iters, args.threshold, 1.0, rescale_depth=True,
                         norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused,
                         keypoints=None if kp is None else (kp, [args.keypoints] * B),
-                        overlap_ref=bool(args.overlap_ref))
+                        overlap_ref=False if args.overlap_ref == "0" else args.overlap_ref)
 
     # --pipeline: step i's sweep (side stream) overlaps step i+1's pose stage
     stepf = hp.step_pipelined if args.pipeline else hp.step
@@ -488,7 +489,7 @@ def _main_gpu(args, dist):
         2.0 ** -15 <= args.threshold < 1.0
     h, w = fhw
     s = 4 if cost_dtype == torch.float32 else 2
-    if args.overlap_ref:
+    if args.overlap_ref != "0":
         # the sweep kernel writes the warped half (and reads tgt); the reference
         # half (writes + its padded ref reads) is k_ref_planes' on the side stream
         sweep_bytes = B * (C * args.nlabel * h * w * s + C * h * w * 4)
@@ -522,7 +523,7 @@ def _main_gpu(args, dist):
                                     f"nlabel={args.nlabel}, C=32 at {h}x{w}, {args.cost_dtype} cost volume"),
                        "pairs_per_gpu": B, "global_batch": world * B, "parallelism": f"dp{world}",
                        "streams": "sweep on a side stream (overlaps the next step's solve)" if args.pipeline
-                       else ("reference half on a side stream beside the scorer" if args.overlap_ref
+                       else (f"reference half on a side stream ({args.overlap_ref})" if args.overlap_ref != "0"
                              else "one stream")},
             "dist": {"world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
                      "backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
@@ -542,7 +543,7 @@ def _main_gpu(args, dist):
                                      "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                      "note": "runs concurrently with k_score_mf2: its duration includes sharing "
                                              "the CUs with the scorer; not on the step's critical path"}
-                                    if args.overlap_ref and "ref_planes" in kt else None),
+                                    if args.overlap_ref != "0" and "ref_planes" in kt else None),
             "solve": {"hypotheses_per_launch": hyps, "ms": round(kt_all["ransac_solve"], 4),
                       "hypotheses_per_s": round(hyps / (kt_all["ransac_solve"] * 1e-3), 1)},
             "kernel_ms": {k: round(v, 4) for k, v in {**kt_all, **kt}.items()},

@@ -73,6 +73,10 @@
 #ifndef SFM_MF2_EXP
 #define SFM_MF2_EXP 0
 #endif
+// the tile loop's fragment addresses from one lane base per two tiles
+#ifndef SFM_MF2_LN1
+#define SFM_MF2_LN1 1
+#endif
 #ifndef SFM_MF2_BPRE
 #define SFM_MF2_BPRE 0
 #endif
@@ -577,12 +581,21 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           zA = mf2_z(mf2_load_d(fr, mf2_lane()), NL, NH, aA);
 #pragma unroll 1
           for (int t = 1; t < kMf2Tiles - 1; t += 2) {
-            aA = mf2_a(mf2_load_ab(fr + (size_t)(t + 1) * kTileHalves, mf2_lane()), A1, A2);
-            zB = mf2_z(mf2_load_d(fr + (size_t)t * kTileHalves, mf2_lane()), NL, NH, aB);
+#if SFM_MF2_LN1
+            // one lane address per two tiles: the four fragment loads use
+            // immediate offsets from it (round 3 recomputed it per load)
+            const int ln = mf2_lane();
+#define MF2_LN ln
+#else
+#define MF2_LN mf2_lane()
+#endif
+            aA = mf2_a(mf2_load_ab(fr + (size_t)(t + 1) * kTileHalves, MF2_LN), A1, A2);
+            zB = mf2_z(mf2_load_d(fr + (size_t)t * kTileHalves, MF2_LN), NL, NH, aB);
             mf2_signs(zA, s1, s2);
-            aB = mf2_a(mf2_load_ab(fr + (size_t)(t + 2) * kTileHalves, mf2_lane()), A1, A2);
-            zA = mf2_z(mf2_load_d(fr + (size_t)(t + 1) * kTileHalves, mf2_lane()), NL, NH, aA);
+            aB = mf2_a(mf2_load_ab(fr + (size_t)(t + 2) * kTileHalves, MF2_LN), A1, A2);
+            zA = mf2_z(mf2_load_d(fr + (size_t)(t + 1) * kTileHalves, MF2_LN), NL, NH, aA);
             mf2_signs(zB, s1, s2);
+#undef MF2_LN
           }
           zB = mf2_z(mf2_load_d(fr + (size_t)(kMf2Tiles - 1) * kTileHalves, mf2_lane()), NL, NH, aB);
           mf2_signs(zA, s1, s2);

@@ -69,8 +69,11 @@ class TwoViewHotPath:
         self.cost_dtype = cost_dtype
         self.sweep_ws = sweep.workspace_for(B, self.C, self.h, self.w, self.device)
         # overlap_ref: the volume's pose-independent reference half on a side
-        # stream beside the scorer (see step_overlap)
-        self.overlap_ref = bool(overlap_ref)
+        # stream (see step_overlap): "score" (or True) beside the RANSAC scorer,
+        # behind the score fence; "step" from the start of the step
+        if overlap_ref not in (False, True, "score", "step"):
+            raise ValueError("overlap_ref must be False, True, 'score' or 'step'")
+        self.overlap_ref = {False: None, True: "score"}.get(overlap_ref, overlap_ref)
         if self.overlap_ref:
             self.ref_ws = sweep.ref_planes_workspace_for(B, self.C, self.h, self.w, self.device)
             self.ref_stream = torch.cuda.Stream(device=self.device)
@@ -141,7 +144,8 @@ class TwoViewHotPath:
         Kinv = self.k_inverse(K)
         E, P, inl, win = self.pose(flow, K, Kinv)
         with torch.cuda.stream(side):
-            _lib.check(_lib.load().sfm_score_fence_wait(_lib.stream_ptr(self.device)), "sfm_score_fence_wait")
+            if self.overlap_ref == "score":
+                _lib.check(_lib.load().sfm_score_fence_wait(_lib.stream_ptr(self.device)), "sfm_score_fence_wait")
             sweep.plane_sweep_ref_half(ref_fea, self.L, self.cost, self.ref_ws)
         ref_fea.record_stream(side)
         cost = sweep.plane_sweep_cost_psnet(ref_fea, tgt_fea, P, K, Kinv, self.L, self.min_depth, self.rescale,

@@ -28,9 +28,12 @@ def test_pipelined_steps_equal_plain_steps(cuda):
     assert torch.equal(plain.cost, piped.cost)            # the last step's volume
 
 
-@pytest.mark.parametrize("dtype,fhw,L", [(torch.float32, (94, 311), 32), (torch.bfloat16, (94, 311), 16),
-                                          (torch.float32, (20, 30), 8), (torch.float32, (12, 17), 5)])
-def test_overlapped_reference_half_equals_full_sweep(cuda, dtype, fhw, L):
+@pytest.mark.parametrize("dtype,fhw,L,mode", [(torch.float32, (94, 311), 32, "score"),
+                                               (torch.bfloat16, (94, 311), 16, "score"),
+                                               (torch.float32, (94, 311), 16, "step"),
+                                               (torch.float32, (20, 30), 8, "score"),
+                                               (torch.float32, (12, 17), 5, "step")])
+def test_overlapped_reference_half_equals_full_sweep(cuda, dtype, fhw, L, mode):
     """step_overlap: the reference half from sfm_plane_sweep_ref_planes on a
     side stream behind the score fence, the warped half from
     sfm_plane_sweep_psnet_warped_half.  Steps back to back; the volume must
@@ -46,7 +49,7 @@ def test_overlapped_reference_half_equals_full_sweep(cuda, dtype, fhw, L):
         steps.append((flow, K, ref, tgt))
     mk = lambda ov: TwoViewHotPath(B, (376, 1242), fhw, C, L, 2, 1e-4, 1.0, True, 0.6, cost_dtype=dtype,
                                    device=cuda, overlap_ref=ov)
-    plain, over = mk(False), mk(True)
+    plain, over = mk(False), mk(mode)
     for a in steps:
         over.cost.fill_(float("nan"))                       # every element must be written this step
         E2, P2, i2, c2 = over.step(*a)
