@@ -100,7 +100,7 @@ const TuneKey kTuneKeys[] = {
     {"solve_lanes", &sfm::Tuning::solve_lanes, v_1_16},
     {"solve_coop", &sfm::Tuning::solve_coop, v_01},
     {"roots_lanes", &sfm::Tuning::roots_lanes, [](int v) { return v >= 1 && v <= 32; }},   // LDS stack columns
-    {"roots_split", &sfm::Tuning::roots_split, [](int v) { return v == 0 || v == 1; }},
+    {"roots_split", &sfm::Tuning::roots_split, [](int v) { return v >= 0 && v <= 2; }},
     {"sweep_lane_pixels", &sfm::Tuning::sweep_lane_pixels, [](int v) { return v >= 0 && v <= 2; }},
     {"sweep_items_per_block", &sfm::Tuning::sweep_items_per_block,
      [](int v) { return v == 1 || v == 2 || v == 4 || v == 8; }},

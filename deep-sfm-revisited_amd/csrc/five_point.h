@@ -1082,17 +1082,24 @@ __device__ __forceinline__ void isolate_r(const SturmR& S, double lo, double hi,
 // roots are written to their slot, so the roots are bit-identical to
 // isolate_r's (tests/test_gpu_roots_split.py: the whole workspace).
 // ---------------------------------------------------------------------------
-constexpr int kRootTasks = kStkLanes * 10;   // a hypothesis has at most 10 isolated roots
-struct RootsShared {                         // one wave's LDS (k_roots_split: one wave per block)
-  double seq[kSturmRegs][kStkLanes];         // each hypothesis' Sturm sequence (s[0] = c[0..10])
-  int np[kStkLanes];
-  double tmn[kRootTasks], tmx[kRootTasks];   // single-root nodes: interval
-  int tatlo[kRootTasks];                     // sign changes at its low end
-  int tmeta[kRootTasks];                     // owner lane | ioff << 8
-  int dlist[kRootTasks];                     // nodes for sbisect's bisection (phase 3)
-  double roots[10][kStkLanes];               // root slots (scaled), 0 where none is found
+// NL hypothesis lanes share one task pool: kStkLanes (one wave per block,
+// roots_split = 1) or kStkLanes x the block's waves (roots_split = 2, the
+// cross-wave pool: phases 2 and 3 are claimed by all the block's waves)
+template <int NL>
+struct RootsSharedT {
+  static constexpr int kTasks = NL * 10;    // a hypothesis has at most 10 isolated roots
+  double seq[kSturmRegs][NL];               // each hypothesis' Sturm sequence (s[0] = c[0..10])
+  int np[NL];
+  double tmn[kTasks], tmx[kTasks];          // single-root nodes: interval
+  int tatlo[kTasks];                        // sign changes at its low end
+  int tmeta[kTasks];                        // owner | ioff << 8 (owner: block hypothesis lane < 256)
+  int dlist[kTasks];                        // nodes for sbisect's bisection (phase 3)
+  double roots[10][NL];                     // root slots (scaled), 0 where none is found
   int ntask, ndl;
+  int next2, next3;                         // pooled claims of phases 2 / 3 (LDS atomics)
 };
+using RootsShared = RootsSharedT<kStkLanes>;
+static_assert(4 * kStkLanes <= 256, "owner lanes fit tmeta's 8 bits");
 
 // isolate_p1's work stack: IsoStack with the four small integers packed in one
 // word (sign-change counts and slots <= 10, depth <= kMaxDepth + 1)
@@ -1107,8 +1114,10 @@ struct IsoStackP {
 };
 
 // phase 1: isolate_r's multi-root bisections; single-root nodes become tasks
+// (`lane`: the hypothesis' owner index in the pool, its stack pre-offset)
+template <class SH>
 __device__ __forceinline__ void isolate_p1(const SturmR& S, double lo, double hi, int atlo, int athi,
-                                           const IsoStackP& stk, RootsShared& sh, int lane) {
+                                           const IsoStackP& stk, SH& sh, int lane) {
   int sp = 0;
   stk.put(sp++, lo, hi, atlo, athi, 0, 0);
   bool bis = false;
@@ -1164,8 +1173,11 @@ __device__ __forceinline__ void isolate_p1(const SturmR& S, double lo, double hi
 }
 
 // phase 2: modrf (sturm.cu:208-275) and modrf_pos's loop (43-205) over the
-// wave's task list, on every lane
-__device__ __forceinline__ void falsi_tasks(RootsShared& sh, int lane) {
+// task list, on every lane.  POOL: the list is the block's (every wave of the
+// block claims from it through an LDS counter); else the wave's own.  A node
+// writes its root to a fixed slot, so who claims it changes no result.
+template <bool POOL, class SH>
+__device__ __forceinline__ void falsi_tasks(SH& sh, int lane) {
   const int ntask = sh.ntask;
   int next = 0, cur = -1, it = 0, owner = 0, ioff = 0;
   bool inv = false;
@@ -1176,12 +1188,17 @@ __device__ __forceinline__ void falsi_tasks(RootsShared& sh, int lane) {
   for (;;) {
     const unsigned long long idle = __ballot(cur < 0);
     const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(idle >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)idle, 0u));
+    if (POOL) {
+      int b0 = 0;
+      if (lane == 0 && idle) b0 = atomicAdd(&sh.next2, __popcll(idle));
+      next = __builtin_amdgcn_readfirstlane(b0);          // every lane is active here: lane 0 is the first
+    }
     bool fresh = false;
     if (cur < 0 && next + rank < ntask) {
       cur = next + rank;
       fresh = true;
     }
-    next += __popcll(idle);
+    if (!POOL) next += __popcll(idle);
     if (__ballot(cur >= 0) == 0ull) break;
     if (fresh) {
       const int m = sh.tmeta[cur];
@@ -1288,7 +1305,8 @@ __device__ __forceinline__ void falsi_tasks(RootsShared& sh, int lane) {
 // would reach it, so the walk down the tree (the stop tests, the sign-change
 // decision, the iteration limit) reproduces the sequential bisection's
 // steps and its final midpoint bit for bit, three steps per pass.
-__device__ __forceinline__ void bisect_deferred(RootsShared& sh, int lane) {
+template <bool POOL, class SH>
+__device__ __forceinline__ void bisect_deferred(SH& sh, int lane) {
   const int ndl = sh.ndl;
   if (ndl == 0) return;
   const int j = lane & 7, gbase = lane & ~7;
@@ -1298,6 +1316,11 @@ __device__ __forceinline__ void bisect_deferred(RootsShared& sh, int lane) {
   for (;;) {
     // the leader (j == 0) of each idle group claims the next node, in group order
     const unsigned long long idle = __ballot(cur < 0 && j == 0);
+    if (POOL) {
+      int b0 = 0;
+      if (lane == 0 && idle) b0 = atomicAdd(&sh.next3, __popcll(idle));
+      next = __builtin_amdgcn_readfirstlane(b0);
+    }
     const unsigned long long below = gbase == 0 ? 0ull : (idle & ((1ull << gbase) - 1ull));
     const int t = next + __popcll(below);
     if (cur < 0 && t < ndl) {
@@ -1312,7 +1335,7 @@ __device__ __forceinline__ void bisect_deferred(RootsShared& sh, int lane) {
       for (int i = 0; i < kSturmRegs; ++i) T.c[i] = sh.seq[i][owner];
       T.np = sh.np[owner];
     }
-    next += __popcll(idle);
+    if (!POOL) next += __popcll(idle);
     if (__ballot(cur >= 0) == 0ull) break;
     // this lane's node: its interval down the heap path from [mn, mx]
     double lo = mn, hi = mx;
@@ -1433,9 +1456,9 @@ __device__ __forceinline__ int count_real_roots_r(const SturmR& R, int* atneg, i
 // of the split isolation (isolate_p1; the roots are completed by phases 2-3
 // in sh and scaled by the caller with *fac_out); R is left holding the
 // sequence for phase 3.
-template <bool SPLIT>
+template <bool SPLIT, class SH = RootsShared>
 __device__ __forceinline__ int real_roots_t(const double poly[11], double roots[10], const IsoStack& stk, SturmR& R,
-                                            RootsShared* sh, const IsoStackP* stk_p, int lane, double* fac_out) {
+                                            SH* sh, const IsoStackP* stk_p, int lane, double* fac_out) {
 #ifdef SFM_ROOTS_STATS
   unsigned long long ts = __builtin_amdgcn_s_memtime();
 #endif
@@ -1548,7 +1571,7 @@ __device__ __forceinline__ int real_roots_t(const double poly[11], double roots[
 
 __device__ __forceinline__ int real_roots_r(const double poly[11], double roots[10], const IsoStack& stk) {
   SturmR R;
-  return real_roots_t<false>(poly, roots, stk, R, nullptr, nullptr, 0, nullptr);
+  return real_roots_t<false, RootsShared>(poly, roots, stk, R, nullptr, nullptr, 0, nullptr);
 }
 
 // null_space_solve_3x3_half_pivot (essential_matrix_5pt.cu:476-507)

@@ -1864,23 +1864,30 @@ __global__ __launch_bounds__(256) void k_fill_cands(const double* __restrict__ E
 }
 
 // k_roots with the split isolation (five_point.h, isolate_p1 / falsi_tasks /
-// bisect_deferred): lanes [0, lanes) own one hypothesis each through phase 1
-// and 3; all 64 lanes share the wave's falsi tasks in phase 2.  One wave per
-// block, so the block barriers are wave barriers.
-__global__ __launch_bounds__(64) void k_roots_split(int H, int lanes, double* __restrict__ st, size_t stride,
-                                                    int32_t* __restrict__ out_nroots) {
+// bisect_deferred): lanes [0, lanes) of each wave own one hypothesis each
+// through phase 1; phases 2 and 3 run over a task list on every lane.  NW = 1
+// (roots_split 1): one wave per block and its own list, so the launch lasts as
+// long as its busiest wave (profiles/r03_roots_split_stats.txt: 245 k cycles
+// per wave on average, 313-325 k at most).  NW = 4 (roots_split 2, default):
+// the block's four waves append to and claim from one pool (LDS counters), so
+// the tail averages over four waves' tasks.  Phase 1 stays per hypothesis, and
+// every node's root goes to its fixed slot: the workspace is byte-identical.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_roots_split(int H, int lanes, double* __restrict__ st, size_t stride,
+                                                         int32_t* __restrict__ out_nroots) {
   const int b = blockIdx.y;
-  const int lane = (int)threadIdx.x;
-  const int h = blockIdx.x * lanes + lane;
+  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  const int h = (blockIdx.x * NW + wv) * lanes + lane;
   const bool own = lane < lanes && h < H;
-  __shared__ double s_lohi[kStkDepth * 2 * kStkLanes];
-  __shared__ int s_meta[kStkDepth * kStkLanes];
-  __shared__ RootsShared sh;
+  const int owner = wv * kStkLanes + lane;                  // the hypothesis' slot in the pool
+  __shared__ double s_lohi[NW][kStkDepth * 2 * kStkLanes];
+  __shared__ int s_meta[NW][kStkDepth * kStkLanes];
+  __shared__ RootsSharedT<kStkLanes * NW> sh;
   if (lane < kStkLanes) {
 #pragma unroll
-    for (int i = 0; i < 10; ++i) sh.roots[i][lane] = 0.0;
+    for (int i = 0; i < 10; ++i) sh.roots[i][owner] = 0.0;
   }
-  if (lane == 0) { sh.ntask = 0; sh.ndl = 0; }
+  if (threadIdx.x == 0) { sh.ntask = 0; sh.ndl = 0; sh.next2 = 0; sh.next3 = 0; }
   __syncthreads();
 #ifdef SFM_ROOTS_STATS
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -1895,8 +1902,8 @@ __global__ __launch_bounds__(64) void k_roots_split(int H, int lanes, double* __
     double roots[10];
     SturmR R;
     const IsoStack stk{nullptr, nullptr};
-    const IsoStackP stkp{s_lohi + lane, s_meta + lane};
-    nr = real_roots_t<true>(poly, roots, stk, R, &sh, &stkp, lane, &fac);
+    const IsoStackP stkp{s_lohi[wv] + lane, s_meta[wv] + lane};
+    nr = real_roots_t<true>(poly, roots, stk, R, &sh, &stkp, owner, &fac);
   }
 #ifdef SFM_ROOTS_STATS
   // split stats: cycles at the end of phase 1 / phase 2 in the second half of g_roots_cycles / g_roots_phase[0]
@@ -1904,17 +1911,17 @@ __global__ __launch_bounds__(64) void k_roots_split(int H, int lanes, double* __
   if (own) g_roots_cycles[si + (1 << 16)] = __builtin_amdgcn_s_memtime() - t0;
 #endif
   __syncthreads();
-  falsi_tasks(sh, lane);
+  falsi_tasks<(NW > 1)>(sh, lane);
   __syncthreads();
 #ifdef SFM_ROOTS_STATS
   if (own) g_roots_phase[0][si] = __builtin_amdgcn_s_memtime() - t0;
 #endif
-  bisect_deferred(sh, lane);
+  bisect_deferred<(NW > 1)>(sh, lane);
   __syncthreads();
   if (own) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-      double r = sh.roots[i][lane];
+      double r = sh.roots[i][owner];
       if (i < nr) r /= fac;
       st_at(st, stride, kStRoots + i, hb) = r;
     }
@@ -1959,8 +1966,11 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     else
       hipLaunchKernelGGL((k_solve_front<Src, false>), dim3((H + lanes - 1) / lanes, bc), dim3(64), 0, s, src, pp, H,
                          seed, lanes, w.sstate, stride);
-    if (tuning().roots_split)
-      hipLaunchKernelGGL(k_roots_split, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate,
+    if (tuning().roots_split == 2)
+      hipLaunchKernelGGL(k_roots_split<4>, dim3((H + 4 * rlanes - 1) / (4 * rlanes), bc), dim3(256), 0, s, H, rlanes,
+                         w.sstate, stride, w.nroots);
+    else if (tuning().roots_split)
+      hipLaunchKernelGGL(k_roots_split<1>, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate,
                          stride, w.nroots);
     else
       hipLaunchKernelGGL(k_roots, dim3((H + rlanes - 1) / rlanes, bc), dim3(64), 0, s, H, rlanes, w.sstate, stride,
