@@ -47,10 +47,6 @@ report("sweep (GPU vs oracle)", cost_gpu, cost_cpu)
 cls_cpu = OR.regularize_fp32(m, cost_cpu)
 cls_gpu = m.to(dev)(cost_cpu.to(dev), precision="fp32").cpu()
 report("regularize fp32 (same cost)", cls_gpu, cls_cpu)
-# layer by layer on the GPU vs CPU, same inputs
-x_cpu = cost_cpu
-for name in ("dres0", "dres1", "dres2", "dres3", "dres4", "classify"):
-    pass
 dep_cpu = S.depth_head(cls_cpu, L, 1.0, out_hw=hw)
 dep_gpu = depth_head(cls_cpu.to(dev), L, 1.0, out_hw=hw).cpu()
 report("depth head (same logits)", dep_gpu, dep_cpu)

@@ -180,3 +180,29 @@ def test_lowp_template_oracle_matches_numpy(prec):
             assert np.array_equal(a, b), (thr, int((a != b).sum()))
             differs += int((a != R.inlier_mask(E, q, qp, thr, prec - 1)).sum())
     assert prec == 33 or differs > 0
+
+
+def test_psnet64_fixture_clear_of_border_step_and_oracle_chain(golden):
+    """psnet64.npz (the float64 depth bar): every plane-sweep sample stays
+    PSNET64_MARGIN clear of the reference's border step (inverse_warp.py:60-66,
+    a sample beyond |xn| = 1 is zeroed, so a float32 rounding near it moves
+    the depth by percent) and the torch-CPU oracle chain (sweep -> the
+    reference's module forward -> head) meets the GPU test's bars against the
+    float64 depth: median <= 1e-5, max <= 1e-4 relative."""
+    from oracle import regularize as OR
+    from oracle.gen_golden import PSNET64_MARGIN, sweep_boundary_margin
+    from sfm_amd.regularize import CostRegularization
+    g = golden("psnet64.npz")
+    inp = g["input"]
+    L = int(inp["nlabel"])
+    H, W = (int(x) for x in inp["image_hw"])
+    m = sweep_boundary_margin(inp["K"], inp["pose_rescaled"][:, 0], L, H // 4, W // 4)
+    assert m >= PSNET64_MARGIN and m == float(inp["boundary_margin"])
+    mod = CostRegularization(64)
+    mod.load_state_dict({k: torch.from_numpy(v) for k, v in g["state"].items()})
+    t = lambda k: torch.from_numpy(inp[k])
+    cost = S.plane_sweep_cost(t("ref_fea"), t("tgt_fea"), t("pose_rescaled")[:, 0], t("K"), t("Kinv"), L, 1.0)
+    dep = S.depth_head(OR.regularize_fp32(mod, cost), L, 1.0, out_hw=(H, W))
+    want = torch.from_numpy(g["out64"]["depth"]).double()
+    r = ((dep.double() - want).abs() / want.abs()).flatten()
+    assert float(r.median()) <= 1e-5 and float(r.max()) <= 1e-4, (float(r.median()), float(r.max()))
