@@ -14,7 +14,7 @@ struct Tuning {
   int solve_lanes = 16;          // active lanes per k_solve_front wave (1..16: LDS records)
   int solve_coop = 1;            // k_solve_front's reduction on DPP quads (4 lanes per hypothesis); 0: one lane
   int roots_lanes = 32;          // active lanes per k_roots wave (1..32: LDS stack columns)
-  int roots_split = 2;           // 2: k_roots_split<4> (one task pool for a block's 4 waves); 1: per wave; 0: k_roots
+  int roots_split = 1;           // 1: k_roots_split (per-wave task pool); 2: k_roots_split<4> (a block's 4 waves, slower); 0: k_roots
   int sweep_items_per_block = 4; // consecutive (row, plane, window) items per sweep block
   int sweep_lane_pixels = 0;     // 1: warped lanes own 4 consecutive pixels (16-byte stores)
   int sweep_flat = 2;            // 1: 256-byte-aligned slab windows (k_sweep_flat); 2: narrow windows (k_sweep_tile); 0: per-row

@@ -1084,7 +1084,10 @@ __device__ __forceinline__ void isolate_r(const SturmR& S, double lo, double hi,
 // ---------------------------------------------------------------------------
 // NL hypothesis lanes share one task pool: kStkLanes (one wave per block,
 // roots_split = 1) or kStkLanes x the block's waves (roots_split = 2, the
-// cross-wave pool: phases 2 and 3 are claimed by all the block's waves)
+// cross-wave pool: phases 2 and 3 are claimed by all the block's waves; it
+// measured 2-6 % slower than per-wave pools, profiles/r04_roots_pool_ab.txt;
+// the cause is not isolated -- the LDS counters are shared by four waves, and
+// a CU holds one such block instead of four independent ones)
 template <int NL>
 struct RootsSharedT {
   static constexpr int kTasks = NL * 10;    // a hypothesis has at most 10 isolated roots

@@ -73,9 +73,10 @@
 #ifndef SFM_MF2_EXP
 #define SFM_MF2_EXP 0
 #endif
-// the tile loop's fragment addresses from one lane base per two tiles
+// the tile loop's fragment addresses from one lane base per two tiles (1;
+// measured 0.8 % slower than the lane id per tile, 0: profiles/r04_mf2_ln1_ab.txt)
 #ifndef SFM_MF2_LN1
-#define SFM_MF2_LN1 1
+#define SFM_MF2_LN1 0
 #endif
 #ifndef SFM_MF2_BPRE
 #define SFM_MF2_BPRE 0

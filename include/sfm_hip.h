@@ -395,9 +395,9 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     k_score_mf2, 1: k_score_mf, 0: VALU scorers;
  *                                     2 by default; exact by proof, same counts)
  *     "roots_split"           0, 1, 2 k_roots_split: falsi nodes shared by the wave's
- *                                     64 lanes (1), or by the four waves of a block
- *                                     (2, default), speculated fallback bisection;
- *                                     same bits as k_roots (0)
+ *                                     64 lanes (1, default), or by the four waves of
+ *                                     a block (2, measured 2-6 % slower), speculated
+ *                                     fallback bisection; same bits as k_roots (0)
  *     "score_mfma"            0, 1    f32 matrix-core scorer k_score_mx (0; exact, slower)
  *     "conv_rolling"          0, 1    rolling-plane Conv3d for cin 32 (1; same bits)
  *

@@ -206,3 +206,20 @@ def test_psnet64_fixture_clear_of_border_step_and_oracle_chain(golden):
     want = torch.from_numpy(g["out64"]["depth"]).double()
     r = ((dep.double() - want).abs() / want.abs()).flatten()
     assert float(r.median()) <= 1e-5 and float(r.max()) <= 1e-4, (float(r.median()), float(r.max()))
+
+
+def test_lowp_template_half_overflow_makes_every_point_an_inlier():
+    """The literal ComputeError<half> with the reference's double Ematrix:
+    an unnormalised candidate (|E| in the hundreds, as 5-point roots give)
+    overflows half's 65504 in d = sqrt(Ex0^2 + ...), so error = xEx / inf = 0
+    and every point counts as an inlier -- the C5 sweep's degenerate winners
+    (DESIGN.md §2.3).  The held-in-T form scales E by a power of two first and
+    is scale-invariant."""
+    rng = np.random.default_rng(0)
+    q = rng.uniform(-0.5, 0.5, (1000, 2))
+    qp = rng.uniform(-0.5, 0.5, (1000, 2))
+    E = rng.normal(size=(3, 3))
+    assert not R.inlier_mask_numpy_tpl(E, q, qp, 1e-4, 17).any()
+    assert R.inlier_mask_numpy_tpl(E * 1000, q, qp, 1e-4, 17).mean() > 0.99
+    assert np.array_equal(R.inlier_mask(E * 1000, q, qp, 1e-4, 17), R.inlier_mask_numpy_tpl(E * 1000, q, qp, 1e-4, 17))
+    assert np.array_equal(R.inlier_mask(E * 1000, q, qp, 1e-4, 16), R.inlier_mask(E, q, qp, 1e-4, 16))
