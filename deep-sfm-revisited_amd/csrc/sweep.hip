@@ -385,6 +385,7 @@ struct FlatGeom {
   int store_nt;    // k_sweep_tile fast path: non-temporal volume stores (tuning key sweep_store_nt)
   int write_ref;   // k_sweep_tile: write the reference rows too (0: the warped half only, the reference
                    // half comes from k_ref_planes, e.g. on a side stream beside RANSAC)
+  int store_px;    // bf16 fast path: consecutive pixels per lane store (tuning key sweep_store_px; 0: pairs)
   unsigned pair_bytes;   // one pair's output volume in bytes (buffer range)
   Magic mwin, mgrp, mhw;
   float inv_w;
@@ -616,6 +617,14 @@ template <typename OutT> struct TileLanes;
 template <> struct TileLanes<float> { static constexpr int AM = 63; };
 template <> struct TileLanes<unsigned short> { static constexpr int AM = 127; };
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void sweep_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ unsigned bf16_pair_swap(unsigned a, unsigned b, bool odd) {
   // a, b: this lane's bf16 of pixel registers 2s and 2s+1; returns the pair
   // (lo, hi) this lane stores: even lane (a_self, a_next), odd (b_prev, b_self)
@@ -654,14 +663,18 @@ __device__ __forceinline__ void sweep_tile_item(const float* __restrict__ ref, c
     ls[j] = l;
   }
   const int nc = min(G, g.C - c0);
-  float cp[G][NJ];
-  if (g.ref_rows && g.write_ref) {
+  constexpr bool LATE = NJ >= 8;                      // reference rows loaded at their stores (registers)
+  float cp[LATE ? 1 : G][NJ];
+  auto load_ref_row = [&](int c, float* v) {
+    const float* R = ref + ((size_t)b * g.C + c0 + c) * g.hw;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) v[j] = *at_u32(R, (unsigned)ps[j] * 4u);
+  };
+  if (!LATE && g.ref_rows && g.write_ref) {
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       if (c >= nc) break;
-      const float* R = ref + ((size_t)b * g.C + c0 + c) * g.hw;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) cp[c][j] = *at_u32(R, (unsigned)ps[j] * 4u);
+      load_ref_row(c, cp[LATE ? 0 : c]);
     }
   }
   Proj pr;
@@ -741,7 +754,8 @@ __device__ __forceinline__ void sweep_tile_item(const float* __restrict__ ref, c
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       if (c >= nc) break;
-      store_row(out + ((size_t)b * g.rows + c0 + c) * (size_t)g.slab, cp[c]);
+      if (LATE) load_ref_row(c, cp[0]);
+      store_row(out + ((size_t)b * g.rows + c0 + c) * (size_t)g.slab, cp[LATE ? 0 : c]);
     }
   }
 #pragma unroll
@@ -772,7 +786,7 @@ __device__ __forceinline__ unsigned next_lane_u(unsigned v) {
 }
 __device__ __forceinline__ float next_lane_f(float v) { return __uint_as_float(next_lane_u(__float_as_uint(v))); }
 
-template <typename OutT, int NQ, int NJ, bool SHARE, bool NT>
+template <typename OutT, int NQ, int NJ, bool SHARE, bool NT, bool WIDE = false>
 __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, const f32x4* __restrict__ tq,
                                                 const Proj* __restrict__ projs, const FlatGeom& g,
                                                 OutT* __restrict__ out, int b, int k, int start) {
@@ -797,15 +811,19 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
   }
   const __amdgpu_buffer_rsrc_t rout = buf_rsrc(out + (size_t)b * g.rows * g.slab, g.pair_bytes);
   const unsigned row_bytes = (unsigned)g.slab * (unsigned)sizeof(OutT);
-  float cp[G][NJ];
-  if (g.ref_rows && g.write_ref) {
-    const __amdgpu_buffer_rsrc_t rref = buf_rsrc(ref + ((size_t)b * g.C + c0) * g.hw, (unsigned)G * g.hw * 4u);
+  // the reference rows: loaded up front (their latency under the sampling),
+  // or, with wide stores (more pixels per lane), row by row at their stores
+  const __amdgpu_buffer_rsrc_t rref = buf_rsrc(ref + ((size_t)b * g.C + c0) * g.hw, (unsigned)G * g.hw * 4u);
+  auto load_ref_row = [&](int c, float* v) {
 #pragma unroll
-    for (int c = 0; c < G; ++c)
+    for (int j = 0; j < NJ; ++j)
+      v[j] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(rref, (unsigned)ps[j] * 4u, (unsigned)c * g.hw * 4u, 0));
+  };
+  float cp[WIDE ? 1 : G][NJ];
+  if (!WIDE && g.ref_rows && g.write_ref) {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        cp[c][j] = __uint_as_float(
-            __builtin_amdgcn_raw_buffer_load_b32(rref, (unsigned)ps[j] * 4u, (unsigned)c * g.hw * 4u, 0));
+    for (int c = 0; c < G; ++c) load_ref_row(c, cp[WIDE ? 0 : c]);
   }
   const Proj pr = projs[b];                    // uniform: scalar loads
   const SampleK sk = sample_consts(g.h, g.w);
@@ -929,7 +947,28 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
   // row r of the pair: soffset r * row_bytes; per-lane byte offset(s) of the window
   auto store_row = [&](unsigned r, const float* v) {
     const unsigned so = r * row_bytes;
-    if (!BF) {
+    if constexpr (WIDE) {
+      // bf16, NJ consecutive pixels per lane store (sweep_store_px): the
+      // register pairs go through a per-wave LDS row (the same 4-byte pairs
+      // as below, at their window positions) and come back as one 8- or
+      // 16-byte store per lane; the gathers stay lane-consecutive
+      static_assert(BF && (NJ == 4 || NJ == 8), "wide stores: bf16, 4 or 8 pixels per lane");
+      __shared__ __attribute__((aligned(16))) uint32_t s_row[kSwThreads / 64][NJ * 32];
+      uint32_t* st = s_row[wave];
+#pragma unroll
+      for (int q = 0; q < NJ / 2; ++q)
+        st[64 * q + (lane >> 1) + (odd ? 32 : 0)] = bf16_pair_swap(to_bf16(v[2 * q]), to_bf16(v[2 * q + 1]), odd);
+      sweep_wave_sync();
+      const unsigned off = (unsigned)(woff + NJ * lane) * 2u;
+      if constexpr (NJ == 8) {
+        const u32x4 x = *reinterpret_cast<const u32x4*>(st + 4 * lane);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rout, off, so, NT ? 3 : 0);
+      } else {
+        const u32x2 x = *reinterpret_cast<const u32x2*>(st + 2 * lane);
+        __builtin_amdgcn_raw_buffer_store_b64(x, rout, off, so, NT ? 3 : 0);
+      }
+      sweep_wave_sync();                        // the row's reads before the next row's writes
+    } else if (!BF) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
         bstore(__float_as_uint(v[j]), rout, (unsigned)(woff + 64 * j + lane) * 4u, so);
@@ -942,9 +981,9 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       }
     }
   };
-  if (g.ref_rows && g.write_ref) {
+  if (!WIDE && g.ref_rows && g.write_ref) {
 #pragma unroll
-    for (int c = 0; c < G; ++c) store_row((unsigned)(c0 + c), cp[c]);
+    for (int c = 0; c < G; ++c) store_row((unsigned)(c0 + c), cp[WIDE ? 0 : c]);
   }
 #pragma unroll
   for (int c = 0; c < G; ++c) {
@@ -952,6 +991,14 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
 #pragma unroll
     for (int j = 0; j < NJ; ++j) v[j] = acc[c >> 2][j][c & 3];
     store_row((unsigned)(g.ref_rows + c0 + c), v);
+  }
+  if (WIDE && g.ref_rows && g.write_ref) {
+#pragma unroll
+    for (int c = 0; c < G; ++c) {
+      float v[NJ];
+      load_ref_row(c, v);
+      store_row((unsigned)(c0 + c), v);
+    }
   }
 }
 
@@ -973,7 +1020,15 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
   if (start >= g.slab) return;
   if (g.buf_ok && start >= 0 && start + WIN <= g.slab && (k + 1) * 4 * NQ <= g.C)
   {
-    if (g.store_nt) {
+    if constexpr (sizeof(OutT) == 2 && (NJ == 4 || NJ == 8)) {
+      if (NJ == 8 || (g.store_px == NJ && !g.share)) {     // NJ = 8 is launched for wide stores only
+        if (g.store_nt) sweep_tile_fast<OutT, NQ, NJ, false, true, true>(ref, tq, projs, g, out, b, k, start);
+        else sweep_tile_fast<OutT, NQ, NJ, false, false, true>(ref, tq, projs, g, out, b, k, start);
+        return;
+      }
+    }
+    if constexpr (NJ == 8) return;
+    else if (g.store_nt) {
       if (g.share) sweep_tile_fast<OutT, NQ, NJ, true, true>(ref, tq, projs, g, out, b, k, start);
       else sweep_tile_fast<OutT, NQ, NJ, false, true>(ref, tq, projs, g, out, b, k, start);
     } else {
@@ -993,7 +1048,10 @@ static void launch_k_sweep_tile_nj(int nj, unsigned blocks, hipStream_t s, const
                                    void* out, const Proj* projs) {
   const dim3 grid(blocks), block(kSwThreads);
   constexpr bool BF = sizeof(OutT) == 2;
-  if (nj >= 4)
+  if (nj >= 8 && BF)
+    hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, (BF ? 8 : 4)>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g,
+                       (OutT*)out, projs);
+  else if (nj >= 4)
     hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, 4>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out, projs);
   else if (nj == 2 || BF)
     hipLaunchKernelGGL((k_sweep_tile<OutT, NQ, 2>), grid, block, 0, s, ref, tq, pose, K4, K4inv, g, (OutT*)out, projs);
@@ -1389,6 +1447,11 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   // k_sweep_tile: 256 * nj elements per window (bf16 packs register pairs: nj even)
   int nj = tuning().sweep_nj;
   if (out_dtype == 1 && nj < 2) nj = 2;
+  // bf16 wide stores: NJ = the pixels per lane store; rows must keep 16-byte
+  // alignment from window to window (slab a multiple of 8 elements)
+  const int store_px = out_dtype == 1 && mode == 2 && slab % 8 == 0 && (uintptr_t)out % 16 == 0 &&
+                       !tuning().sweep_share ? tuning().sweep_store_px : 0;
+  if (store_px) nj = store_px;
   if (mode == 3 && hw < (1 << 24) && slab < ((int64_t)1 << 30)) {
     const int bnj = out_dtype == 1 ? 2 : 1;
     const int esz = out_dtype == 0 ? 4 : 2;
@@ -1448,6 +1511,7 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     fg.share = tuning().sweep_share;
     fg.store_nt = tuning().sweep_store_nt == 2 ? out_dtype != 0 : tuning().sweep_store_nt;   // auto: bf16 only
     fg.write_ref = write_ref ? 1 : 0;
+    fg.store_px = store_px;
     fg.pair_bytes = fg.buf_ok ? (unsigned)pair_bytes : 0u;
     fg.mwin = make_magic((unsigned)nwin);
     fg.mgrp = make_magic((unsigned)fgroups);

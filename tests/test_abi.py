@@ -154,7 +154,7 @@ def test_tuning_keys_round_trip():
     doc = open(os.path.join(ROOT, "include", "sfm_hip.h")).read()
     block = doc[doc.index("Tuning knobs"):doc.index("int sfm_tune_set")]
     keys = re.findall(r'"([a-z0-9_]+)"', block)
-    assert len(set(keys)) == 24 and "score_lowp_template" in keys and "solve_coop" in keys and "score_mf" in keys and "roots_split" in keys and "sweep_buffer" in keys
+    assert len(set(keys)) == 25 and "score_lowp_template" in keys and "solve_coop" in keys and "score_mf" in keys and "roots_split" in keys and "sweep_buffer" in keys
     for k in keys:
         _lib.tune_get(k)
     old = _lib.tune_get("sweep_nj")

@@ -158,3 +158,39 @@ def test_shared_taps_equal_gathered(cuda, dtype, B, C, L, hw, tscale, by_depth):
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
     assert float(outs[0][:, C:].float().abs().sum()) > 0.0
+
+
+@pytest.mark.parametrize("B,C,L,hw,tscale,by_depth", [
+    (4, 32, 128, None, 0.6, False),     # the C3 volume (94x311, RESCALE_DEPTH pose)
+    (1, 32, 64, None, 3.0, True),       # large baseline, depth planes
+    (2, 16, 8, (40, 300), 0.6, False),  # windows across row and plane ends
+    (1, 8, 5, (13, 64), 1.0, False),    # hw < 256: windows span several planes
+    (1, 8, 5, (13, 61), 1.0, False),    # odd slab: wide stores fall back to pairs
+])
+def test_wide_bf16_stores_equal_pairs(cuda, B, C, L, hw, tscale, by_depth):
+    """sweep_store_px = 4 / 8 (bf16: 4 or 8 consecutive pixels per lane store,
+    the register pairs transposed through a per-wave LDS row) writes the same
+    bits as the 4-byte pair stores, with and without non-temporal stores."""
+    from sfm_amd import _lib, synth
+    from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
+    h, w = hw or synth.feature_hw()
+    ref, tgt = synth.features(B, C, h, w, seed=C + L)
+    K = synth.intrinsics(B, 4.0 * w, 4.0 * w, 2.0 * w, 2.0 * h) if hw else synth.intrinsics(B)
+    Ki = torch.inverse(K)
+    pose = synth.relative_pose(B, torch.Generator().manual_seed(L))
+    pose[:, :, 3] *= tscale / pose[:, :, 3].norm(dim=1, keepdim=True)
+    K4, Ki4 = quarter_intrinsics(K, Ki)
+    args = (ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 1.0)
+    old = _lib.tune_get("sweep_store_px"), _lib.tune_get("sweep_store_nt")
+    try:
+        outs = []
+        for px, nt in ((0, 2), (4, 2), (8, 2), (8, 0), (4, 0)):
+            _lib.tune("sweep_store_px", px)
+            _lib.tune("sweep_store_nt", nt)
+            outs.append(plane_sweep_cost(*args, dtype=torch.bfloat16, predict_by_depth=by_depth))
+    finally:
+        _lib.tune("sweep_store_px", old[0])
+        _lib.tune("sweep_store_nt", old[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0].view(torch.int16), o.view(torch.int16))
+    assert float(outs[0][:, C:].float().abs().sum()) > 0.0
