@@ -91,6 +91,9 @@ def parse(argv=None):
                     help="the cost volume's pose-independent reference half on a side stream "
                          "(TwoViewHotPath.step_overlap): 'score' beside the RANSAC scorer (behind the score fence), "
                          "'step' from the start of the step; the sweep after RANSAC then writes the warped half")
+    ap.add_argument("--tune", default="",
+                    help="launch-shape tuning keys for A/B runs, 'key=value,key=value' (sfm_tune_set; "
+                         "include/sfm_hip.h lists them); recorded in config.tune")
     args = ap.parse_args(argv)
     b, hw, it, nl, cd, kp = CONFIGS[args.config]
     args.batch = b if args.batch is None else args.batch
@@ -439,6 +442,9 @@ def _main_gpu(args, dist):
     kp = None
     if args.keypoints:
         kp = synth.keypoints(B, args.keypoints, hw, seed=rank, device=dev)
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _lib.tune(k.strip(), int(v))
     hp = TwoViewHotPath(B, hw, fhw, C, args.nlabel, args.iters, args.threshold, 1.0, rescale_depth=True,
                         norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused,
                         keypoints=None if kp is None else (kp, [args.keypoints] * B),
@@ -524,7 +530,8 @@ def _main_gpu(args, dist):
                        "pairs_per_gpu": B, "global_batch": world * B, "parallelism": f"dp{world}",
                        "streams": "sweep on a side stream (overlaps the next step's solve)" if args.pipeline
                        else (f"reference half on a side stream ({args.overlap_ref})" if args.overlap_ref != "0"
-                             else "one stream")},
+                             else "one stream"),
+                       **({"tune": args.tune} if args.tune else {})},
             "dist": {"world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1,
                      "backend": torch.distributed.get_backend() if torch.distributed.is_initialized() else None,
                      "devices": names},

@@ -619,10 +619,11 @@ template <> struct TileLanes<unsigned short> { static constexpr int AM = 127; };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// a wave's LDS stage handed between its lanes: the compiler keeps every
+// memory access on its side (the "memory" clobber; wavefront-scope fences do
+// not order plain accesses) and the LDS operations before it have completed
 __device__ __forceinline__ void sweep_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 __device__ __forceinline__ unsigned bf16_pair_swap(unsigned a, unsigned b, bool odd) {
@@ -820,10 +821,11 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       v[j] = __uint_as_float(
           __builtin_amdgcn_raw_buffer_load_b32(rref, (unsigned)ps[j] * 4u, (unsigned)c * g.hw * 4u, 0));
   };
-  float cp[WIDE ? 1 : G][NJ];
-  if (!WIDE && g.ref_rows && g.write_ref) {
+  constexpr bool LATE = WIDE && NJ == 8;        // registers: the reference rows at their stores
+  float cp[LATE ? 1 : G][NJ];
+  if (!LATE && g.ref_rows && g.write_ref) {
 #pragma unroll
-    for (int c = 0; c < G; ++c) load_ref_row(c, cp[WIDE ? 0 : c]);
+    for (int c = 0; c < G; ++c) load_ref_row(c, cp[LATE ? 0 : c]);
   }
   const Proj pr = projs[b];                    // uniform: scalar loads
   const SampleK sk = sample_consts(g.h, g.w);
@@ -947,28 +949,7 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
   // row r of the pair: soffset r * row_bytes; per-lane byte offset(s) of the window
   auto store_row = [&](unsigned r, const float* v) {
     const unsigned so = r * row_bytes;
-    if constexpr (WIDE) {
-      // bf16, NJ consecutive pixels per lane store (sweep_store_px): the
-      // register pairs go through a per-wave LDS row (the same 4-byte pairs
-      // as below, at their window positions) and come back as one 8- or
-      // 16-byte store per lane; the gathers stay lane-consecutive
-      static_assert(BF && (NJ == 4 || NJ == 8), "wide stores: bf16, 4 or 8 pixels per lane");
-      __shared__ __attribute__((aligned(16))) uint32_t s_row[kSwThreads / 64][NJ * 32];
-      uint32_t* st = s_row[wave];
-#pragma unroll
-      for (int q = 0; q < NJ / 2; ++q)
-        st[64 * q + (lane >> 1) + (odd ? 32 : 0)] = bf16_pair_swap(to_bf16(v[2 * q]), to_bf16(v[2 * q + 1]), odd);
-      sweep_wave_sync();
-      const unsigned off = (unsigned)(woff + NJ * lane) * 2u;
-      if constexpr (NJ == 8) {
-        const u32x4 x = *reinterpret_cast<const u32x4*>(st + 4 * lane);
-        __builtin_amdgcn_raw_buffer_store_b128(x, rout, off, so, NT ? 3 : 0);
-      } else {
-        const u32x2 x = *reinterpret_cast<const u32x2*>(st + 2 * lane);
-        __builtin_amdgcn_raw_buffer_store_b64(x, rout, off, so, NT ? 3 : 0);
-      }
-      sweep_wave_sync();                        // the row's reads before the next row's writes
-    } else if (!BF) {
+    if (!BF) {                                  // (wide stores: put / flush below)
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
         bstore(__float_as_uint(v[j]), rout, (unsigned)(woff + 64 * j + lane) * 4u, so);
@@ -981,23 +962,74 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       }
     }
   };
-  if (!WIDE && g.ref_rows && g.write_ref) {
+  if constexpr (WIDE) {
+    // 16-byte lane stores (sweep_store_px): a 16-byte store holds EPL pixels
+    // (8 bf16 / 4 fp32) and the wave's window of a row, 64 NJ pixels, takes
+    // LPR = 64 NJ / EPL lanes, so one store instruction covers RPS = 64 / LPR
+    // consecutive rows.  The pixels go through a per-wave LDS stage of RPS
+    // rows (1 KB) at their window positions and come back as EPL consecutive
+    // pixels per lane; the tap gathers stay lane-consecutive.
+    constexpr int EPL = 16 / (int)sizeof(OutT), LPR = 64 * NJ / EPL, RPS = 64 / LPR;
+    static_assert(NJ <= EPL && EPL % NJ == 0, "wide stores: NJ divides the pixels of a 16-byte store");
+    __shared__ __attribute__((aligned(16))) uint32_t s_rows[kSwThreads / 64][RPS][16 * LPR / 4];
+    const int rr = lane / LPR, cl = lane - rr * LPR;
+    const unsigned voff = (unsigned)(woff + EPL * cl) * (unsigned)sizeof(OutT) + (unsigned)rr * row_bytes;
+    // (per-pixel LDS writes: staging the plain path's DPP-packed bf16 pairs as
+    // 4-byte writes gave wrong words at upper-half chunk starts on gfx950 --
+    // scripts/diag_wide.py; the cause was not isolated)
+    auto put = [&](int slot, const float* v) {
+      OutT* st = reinterpret_cast<OutT*>(s_rows[wave][slot]);
 #pragma unroll
-    for (int c = 0; c < G; ++c) store_row((unsigned)(c0 + c), cp[WIDE ? 0 : c]);
-  }
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (BF) st[64 * j + lane] = (unsigned short)to_bf16(v[j]);
+        else st[64 * j + lane] = v[j];
+      }
+    };
+    auto flush = [&](unsigned r0) {             // rows r0 .. r0 + RPS - 1
+      sweep_wave_sync();
+      const u32x4 x = *reinterpret_cast<const u32x4*>(&s_rows[wave][rr][4 * cl]);
+      __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff, r0 * row_bytes, NT ? 3 : 0);
+      sweep_wave_sync();                        // the stage's reads before the next rows' writes
+    };
+    static_assert(G % RPS == 0, "row groups");
 #pragma unroll
-  for (int c = 0; c < G; ++c) {
-    float v[NJ];
+    for (int c = 0; c < G; c += RPS) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) v[j] = acc[c >> 2][j][c & 3];
-    store_row((unsigned)(g.ref_rows + c0 + c), v);
-  }
-  if (WIDE && g.ref_rows && g.write_ref) {
+      for (int t = 0; t < RPS; ++t) {
+        float v[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) v[j] = acc[(c + t) >> 2][j][(c + t) & 3];
+        put(t, v);
+      }
+      flush((unsigned)(g.ref_rows + c0 + c));
+    }
+    if (g.ref_rows && g.write_ref) {
+#pragma unroll
+      for (int c = 0; c < G; c += RPS) {
+#pragma unroll
+        for (int t = 0; t < RPS; ++t) {
+          if (LATE) {
+            float v[NJ];
+            load_ref_row(c + t, v);
+            put(t, v);
+          } else {
+            put(t, cp[LATE ? 0 : c + t]);
+          }
+        }
+        flush((unsigned)(c0 + c));
+      }
+    }
+  } else {
+    if (g.ref_rows && g.write_ref) {
+#pragma unroll
+      for (int c = 0; c < G; ++c) store_row((unsigned)(c0 + c), cp[LATE ? 0 : c]);
+    }
 #pragma unroll
     for (int c = 0; c < G; ++c) {
       float v[NJ];
-      load_ref_row(c, v);
-      store_row((unsigned)(c0 + c), v);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) v[j] = acc[c >> 2][j][c & 3];
+      store_row((unsigned)(g.ref_rows + c0 + c), v);
     }
   }
 }
@@ -1020,7 +1052,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
   if (start >= g.slab) return;
   if (g.buf_ok && start >= 0 && start + WIN <= g.slab && (k + 1) * 4 * NQ <= g.C)
   {
-    if constexpr (sizeof(OutT) == 2 && (NJ == 4 || NJ == 8)) {
+    if constexpr (NJ <= 16 / (int)sizeof(OutT)) {
       if (NJ == 8 || (g.store_px == NJ && !g.share)) {     // NJ = 8 is launched for wide stores only
         if (g.store_nt) sweep_tile_fast<OutT, NQ, NJ, false, true, true>(ref, tq, projs, g, out, b, k, start);
         else sweep_tile_fast<OutT, NQ, NJ, false, false, true>(ref, tq, projs, g, out, b, k, start);
@@ -1447,10 +1479,14 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   // k_sweep_tile: 256 * nj elements per window (bf16 packs register pairs: nj even)
   int nj = tuning().sweep_nj;
   if (out_dtype == 1 && nj < 2) nj = 2;
-  // bf16 wide stores: NJ = the pixels per lane store; rows must keep 16-byte
-  // alignment from window to window (slab a multiple of 8 elements)
-  const int store_px = out_dtype == 1 && mode == 2 && slab % 8 == 0 && (uintptr_t)out % 16 == 0 &&
-                       !tuning().sweep_share ? tuning().sweep_store_px : 0;
+  // 16-byte lane stores: NJ = the tuned pixels per lane (bf16: 2, 4, 8;
+  // fp32: 1, 2, 4); rows keep 16-byte alignment from window to window (slab
+  // a multiple of a store's pixels)
+  int store_px = tuning().sweep_store_px;
+  if (out_dtype == 1 && store_px == 1) store_px = 2;
+  if (out_dtype == 0 && store_px == 8) store_px = 0;
+  if (!(mode == 2 && slab % (out_dtype == 1 ? 8 : 4) == 0 && (uintptr_t)out % 16 == 0 && !tuning().sweep_share))
+    store_px = 0;
   if (store_px) nj = store_px;
   if (mode == 3 && hw < (1 << 24) && slab < ((int64_t)1 << 30)) {
     const int bnj = out_dtype == 1 ? 2 : 1;

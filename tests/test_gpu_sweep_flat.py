@@ -160,17 +160,19 @@ def test_shared_taps_equal_gathered(cuda, dtype, B, C, L, hw, tscale, by_depth):
     assert float(outs[0][:, C:].float().abs().sum()) > 0.0
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B,C,L,hw,tscale,by_depth", [
     (4, 32, 128, None, 0.6, False),     # the C3 volume (94x311, RESCALE_DEPTH pose)
     (1, 32, 64, None, 3.0, True),       # large baseline, depth planes
     (2, 16, 8, (40, 300), 0.6, False),  # windows across row and plane ends
     (1, 8, 5, (13, 64), 1.0, False),    # hw < 256: windows span several planes
-    (1, 8, 5, (13, 61), 1.0, False),    # odd slab: wide stores fall back to pairs
+    (1, 8, 5, (13, 61), 1.0, False),    # odd slab: wide stores fall back to the plain path
 ])
-def test_wide_bf16_stores_equal_pairs(cuda, B, C, L, hw, tscale, by_depth):
-    """sweep_store_px = 4 / 8 (bf16: 4 or 8 consecutive pixels per lane store,
-    the register pairs transposed through a per-wave LDS row) writes the same
-    bits as the 4-byte pair stores, with and without non-temporal stores."""
+def test_wide_stores_equal_plain(cuda, dtype, B, C, L, hw, tscale, by_depth):
+    """sweep_store_px (16-byte lane stores of 8 bf16 / 4 fp32 consecutive
+    pixels, transposed through a per-wave LDS stage, with px pixels per lane
+    for the taps) writes the same bits as the plain 4-byte lane stores, with
+    and without non-temporal stores."""
     from sfm_amd import _lib, synth
     from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
     h, w = hw or synth.feature_hw()
@@ -184,13 +186,22 @@ def test_wide_bf16_stores_equal_pairs(cuda, B, C, L, hw, tscale, by_depth):
     old = _lib.tune_get("sweep_store_px"), _lib.tune_get("sweep_store_nt")
     try:
         outs = []
-        for px, nt in ((0, 2), (4, 2), (8, 2), (8, 0), (4, 0)):
+        if dtype == torch.bfloat16:
+            cases = ((0, 2), (2, 2), (4, 2), (8, 2), (8, 0), (2, 0))
+        else:
+            cases = ((0, 2), (1, 2), (2, 2), (4, 2), (1, 1), (2, 1))
+        for px, nt in cases:
             _lib.tune("sweep_store_px", px)
             _lib.tune("sweep_store_nt", nt)
-            outs.append(plane_sweep_cost(*args, dtype=torch.bfloat16, predict_by_depth=by_depth))
+            outs.append(plane_sweep_cost(*args, dtype=dtype, predict_by_depth=by_depth))
     finally:
         _lib.tune("sweep_store_px", old[0])
         _lib.tune("sweep_store_nt", old[1])
-    for o in outs[1:]:
-        assert torch.equal(outs[0].view(torch.int16), o.view(torch.int16))
+    bad = {}
+    iv = torch.int16 if dtype == torch.bfloat16 else torch.int32
+    for (px, nt), o in zip(cases[1:], outs[1:]):
+        d = (outs[0].view(iv) != o.view(iv)).nonzero()
+        if len(d):
+            bad[(px, nt)] = (len(d), d[:4].tolist())
+    assert not bad, bad
     assert float(outs[0][:, C:].float().abs().sum()) > 0.0
