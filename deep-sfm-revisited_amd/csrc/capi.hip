@@ -108,7 +108,7 @@ const TuneKey kTuneKeys[] = {
     {"sweep_buffer", &sfm::Tuning::sweep_buffer, v_01},
     {"sweep_share", &sfm::Tuning::sweep_share, v_01},
     {"sweep_store_nt", &sfm::Tuning::sweep_store_nt, [](int v) { return v >= 0 && v <= 2; }},
-    {"sweep_store_px", &sfm::Tuning::sweep_store_px, [](int v) { return v == 0 || v == 1 || v == 2 || v == 4 || v == 8; }},
+    {"sweep_store_px", &sfm::Tuning::sweep_store_px, [](int v) { return v >= -1 && v <= 8 && (v <= 2 || v == 4 || v == 8); }},
     {"sweep_run", &sfm::Tuning::sweep_run, [](int v) { return v >= 1 && v <= 1024; }},
     {"sweep_band_rows", &sfm::Tuning::sweep_band_rows, [](int v) { return v >= 2 && v <= 64; }},
     {"sweep_nj", &sfm::Tuning::sweep_nj, [](int v) { return v == 1 || v == 2 || v == 4; }},

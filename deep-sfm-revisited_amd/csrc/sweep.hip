@@ -1482,7 +1482,11 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   // 16-byte lane stores: NJ = the tuned pixels per lane (bf16: 2, 4, 8;
   // fp32: 1, 2, 4); rows keep 16-byte alignment from window to window (slab
   // a multiple of a store's pixels)
+  // default (-1): bf16 volumes 2 pixels per lane (the C3 sweep 0.454 -> 0.347 ms
+  // in the bench step, profiles/r04_sweep_wide_ab.txt), fp32 the plain stores
+  // (write-bound already: 1 pixel per lane equal, 2 slower)
   int store_px = tuning().sweep_store_px;
+  if (store_px < 0) store_px = out_dtype == 1 ? 2 : 0;
   if (out_dtype == 1 && store_px == 1) store_px = 2;
   if (out_dtype == 0 && store_px == 8) store_px = 0;
   if (!(mode == 2 && slab % (out_dtype == 1 ? 8 : 4) == 0 && (uintptr_t)out % 16 == 0 && !tuning().sweep_share))

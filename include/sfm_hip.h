@@ -380,10 +380,11 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *     "sweep_store_nt"        0,1,2   k_sweep_tile's volume stores non-temporal (sc0 nt)
  *                                     so they do not evict the re-read operands
  *                                     (2: bf16 volumes only)
- *     "sweep_store_px"        0,2,4,8 bf16 volumes: 16-byte lane stores (8 consecutive
- *                                     pixels through a per-wave LDS stage, 8 / value
- *                                     rows per store) with that many pixels per lane
- *                                     for the taps; 0: 4-byte pairs; same bits
+ *     "sweep_store_px"        -1,0,1, 16-byte lane stores of k_sweep_tile (8 bf16 / 4
+ *                             2,4,8   fp32 consecutive pixels through a per-wave LDS
+ *                                     stage) with that many pixels per lane for the
+ *                                     taps; 0: plain 4-byte lane stores; -1 (default):
+ *                                     bf16 2, fp32 plain; same bits
  *     "sweep_run"             1..1024 planes per block of k_sweep_band (16)
  *     "sweep_band_rows"       2..64   target rows k_sweep_band stages in LDS (16,
  *                                     clipped to 80 KB per block)

@@ -187,7 +187,7 @@ def test_wide_stores_equal_plain(cuda, dtype, B, C, L, hw, tscale, by_depth):
     try:
         outs = []
         if dtype == torch.bfloat16:
-            cases = ((0, 2), (2, 2), (4, 2), (8, 2), (8, 0), (2, 0))
+            cases = ((0, 2), (-1, 2), (2, 2), (4, 2), (8, 2), (8, 0), (2, 0))
         else:
             cases = ((0, 2), (1, 2), (2, 2), (4, 2), (1, 1), (2, 1))
         for px, nt in cases:
