@@ -324,8 +324,9 @@ def cpu_baseline(flow, K, ref_fea, tgt_fea, pose, args, n_pts=None, keypoints=No
 def regularize_roofline(cost, steps=3, precision="bf16"):
     """PSNet's 12-layer 3-D cost regularisation on the first pair of the last
     step's cost volume, after the timed region: sfm_conv3_bf16 (bf16 MFMA,
-    the fast option) or sfm_conv3_f32 (precision "fp32": f32 MFMA, the
-    reference's precision).  Not part of ``value`` (the metric's path ends at
+    the fast option), sfm_conv3_f16 (precision "fp16": f16 MFMA, the
+    reference's precision under cfg.MIXED_PREC) or sfm_conv3_f32 (precision
+    "fp32": f32 MFMA, the reference's precision).  Not part of ``value`` (the metric's path ends at
     the cost volume); reported so the MFMA kernels' rooflines are measured
     live beside the path's."""
     import torch
@@ -342,13 +343,13 @@ def regularize_roofline(cost, steps=3, precision="bf16"):
         reg(one, precision=precision)
     torch.cuda.synchronize(cost.device)
     _lib.profile_enable(False)
-    ms, n = _lib.profile_read("conv3" if precision == "bf16" else "conv3_f32")
+    ms, n = _lib.profile_read({"bf16": "conv3", "fp16": "conv3_f16", "fp32": "conv3_f32"}[precision])
     _, L, h, w = one.shape[1:]
     vox = L * h * w
     flop = 2 * vox * 27 * (one.shape[1] * 32 + 10 * 32 * 32 + 32)
     per_stack = ms / steps
     tf = flop / (per_stack * 1e-3) / 1e12
-    peak = PEAK_BF16_TFLOPS if precision == "bf16" else PEAK_F32_MFMA_TFLOPS
+    peak = PEAK_F32_MFMA_TFLOPS if precision == "fp32" else PEAK_BF16_TFLOPS   # f16 dense = bf16 dense
     return {"kernel": f"conv3 x12 (PSNet dres0..classify, {precision} MFMA)", "bound": f"mfma-{precision}",
             "achieved": round(tf, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(tf / peak, 4),
             "avg_launch_ms": round(ms / max(n, 1), 4), "ms_per_stack": round(per_stack, 4),
@@ -564,9 +565,10 @@ def _main_gpu(args, dist):
                          "via": "dist.gather_rows (all_gather of E[9], P[12], inliers per pair)"},
         }
         if world == 1 and not args.no_regularize and hp.cost.dtype in (torch.float32, torch.bfloat16):
-            for prec, key in (("bf16", "roofline_regularize"), ("fp32", "roofline_regularize_fp32")):
+            for prec, key in (("bf16", "roofline_regularize"), ("fp16", "roofline_regularize_fp16"),
+                              ("fp32", "roofline_regularize_fp32")):
                 try:
-                    out[key] = regularize_roofline(hp.cost, steps=3 if prec == "bf16" else 2, precision=prec)
+                    out[key] = regularize_roofline(hp.cost, steps=2 if prec == "fp32" else 3, precision=prec)
                 except Exception as e:   # extra information, never the metric
                     out[key] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only

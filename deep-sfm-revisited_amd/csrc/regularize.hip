@@ -55,16 +55,44 @@ __device__ __forceinline__ unsigned short f2bf(float f) {  // RNE (v_cvt_pk_bf16
   return __builtin_bit_cast(unsigned short, v);
 }
 
+// 16-bit activation type of the low-precision stack: bf16 (8-bit mantissa,
+// the fast opt-in) or f16 (11-bit mantissa: what the reference's Conv3d
+// layers compute in under cfg.MIXED_PREC autocast, SFMnet.py:164 with
+// cfgs/kitti.yml:10).  Same tiling; the MFMA and the conversions differ.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <bool F16> struct Act;
+template <> struct Act<false> {
+  using v8 = bf16x8;
+  static __device__ __forceinline__ float to_f(unsigned short b) { return bf2f(b); }
+  static __device__ __forceinline__ unsigned short from_f(float f) { return f2bf(f); }
+  static __device__ __forceinline__ f32x16 mfma(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Act<true> {
+  using v8 = f16x8;
+  static __device__ __forceinline__ float to_f(unsigned short b) { return (float)__builtin_bit_cast(_Float16, b); }
+  static __device__ __forceinline__ unsigned short from_f(float f) {   // RNE (v_cvt_f16_f32)
+    return __builtin_bit_cast(unsigned short, (_Float16)f);
+  }
+  static __device__ __forceinline__ f32x16 mfma(v8 a, v8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+
 // D = W . X: rows = 32 output channels (weights as the A operand), columns =
 // 32 pixels of one output row (the input as the B operand).  A wave owns 4
 // output rows x 32 pixels (4 accumulators); each input row fragment it reads
 // from LDS feeds up to 3 of them (dy = 0, 1, 2), so an MFMA costs 0.5 input
 // and 0.25 weight ds_read_b128.
+template <bool F16>
 __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
     const unsigned short* __restrict__ in, int cin, const unsigned short* __restrict__ wpk,
     const float* __restrict__ scale, const float* __restrict__ bias, const unsigned short* __restrict__ res, int relu,
     unsigned short* __restrict__ out, float* __restrict__ out1, int D, int H, int W, int ntx, int nty, int nblk,
     int per_xcd) {
+  using A = Act<F16>;
+  using v8 = typename A::v8;
   __shared__ __attribute__((aligned(16))) unsigned char lds_in[kInBytes];
   __shared__ __attribute__((aligned(16))) unsigned char lds_w[kWBytes];
   const int tid = threadIdx.x;
@@ -161,19 +189,19 @@ __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
       const int c = kb * 2 + h;
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
-        bf16x8 wf[3], xf[6];
+        v8 wf[3], xf[6];
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
-          wf[dy] = *reinterpret_cast<const bf16x8*>(lds_w + ((dy * 3 + dx) * 32 + r) * 64 + swz(c, r) * 16);
+          wf[dy] = *reinterpret_cast<const v8*>(lds_w + ((dy * 3 + dx) * 32 + r) * 64 + swz(c, r) * 16);
         const int p = wcol + r + dx;
 #pragma unroll
         for (int ir = 0; ir < 6; ++ir)  // input rows wrow .. wrow + 5 of the halo
-          xf[ir] = *reinterpret_cast<const bf16x8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
+          xf[ir] = *reinterpret_cast<const v8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
         // dy-major: consecutive MFMAs update different accumulators
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-          for (int o = 0; o < 4; ++o) acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[dy], xf[o + dy], acc[o], 0, 0, 0);
+          for (int o = 0; o < 4; ++o) acc[o] = A::mfma(wf[dy], xf[o + dy], acc[o]);
       }
     }
   }
@@ -201,14 +229,14 @@ __global__ __launch_bounds__(kConvThreads, SFM_CONV_MINW) void k_conv3(
         for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.0f);
       if (res) {
         const uint2 rv = *reinterpret_cast<const uint2*>(res + pix * 32 + co);
-        v[0] += bf2f(rv.x & 0xffff);
-        v[1] += bf2f(rv.x >> 16);
-        v[2] += bf2f(rv.y & 0xffff);
-        v[3] += bf2f(rv.y >> 16);
+        v[0] += A::to_f(rv.x & 0xffff);
+        v[1] += A::to_f(rv.x >> 16);
+        v[2] += A::to_f(rv.y & 0xffff);
+        v[3] += A::to_f(rv.y >> 16);
       }
       uint2 st;
-      st.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-      st.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+      st.x = (unsigned)A::from_f(v[0]) | ((unsigned)A::from_f(v[1]) << 16);
+      st.y = (unsigned)A::from_f(v[2]) | ((unsigned)A::from_f(v[3]) << 16);
       *reinterpret_cast<uint2*>(out + pix * 32 + co) = st;
     }
   }
@@ -229,6 +257,7 @@ constexpr int kRInBytes = kRHaloY * kHaloX * 64;    // 25,344
 constexpr int kRWBytes = 27 * 32 * 64;              // 55,296
 constexpr int kRLds = kRInBytes + kRWBytes;         // 80,640: two blocks per CU
 
+template <bool F16>
 __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restrict__ in,
                                                    const unsigned short* __restrict__ wpk,
                                                    const float* __restrict__ scale, const float* __restrict__ bias,
@@ -236,6 +265,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
                                                    unsigned short* __restrict__ out, float* __restrict__ out1, int D,
                                                    int H, int W, int ntx, int nty, int ndc, int nplanes, int nblk,
                                                    int per_xcd) {
+  using A = Act<F16>;
+  using v8 = typename A::v8;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   unsigned char* lds_w = lds;
   unsigned char* lds_in = lds + kRWBytes;
@@ -328,14 +359,14 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
           for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.0f);
         if (res) {
           const uint2 rv = *reinterpret_cast<const uint2*>(res + pix * 32 + co);
-          v[0] += bf2f(rv.x & 0xffff);
-          v[1] += bf2f(rv.x >> 16);
-          v[2] += bf2f(rv.y & 0xffff);
-          v[3] += bf2f(rv.y >> 16);
+          v[0] += A::to_f(rv.x & 0xffff);
+          v[1] += A::to_f(rv.x >> 16);
+          v[2] += A::to_f(rv.y & 0xffff);
+          v[3] += A::to_f(rv.y >> 16);
         }
         uint2 st;
-        st.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-        st.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+        st.x = (unsigned)A::from_f(v[0]) | ((unsigned)A::from_f(v[1]) << 16);
+        st.y = (unsigned)A::from_f(v[2]) | ((unsigned)A::from_f(v[3]) << 16);
         *reinterpret_cast<uint2*>(out + pix * 32 + co) = st;
       }
     }
@@ -394,18 +425,18 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
             const unsigned int w4[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              v[8 * k + 2 * e] += bf2f(w4[e] & 0xffff);
-              v[8 * k + 2 * e + 1] += bf2f(w4[e] >> 16);
+              v[8 * k + 2 * e] += A::to_f(w4[e] & 0xffff);
+              v[8 * k + 2 * e + 1] += A::to_f(w4[e] >> 16);
             }
           }
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           uint4 st;
-          st.x = (unsigned)f2bf(v[8 * k + 0]) | ((unsigned)f2bf(v[8 * k + 1]) << 16);
-          st.y = (unsigned)f2bf(v[8 * k + 2]) | ((unsigned)f2bf(v[8 * k + 3]) << 16);
-          st.z = (unsigned)f2bf(v[8 * k + 4]) | ((unsigned)f2bf(v[8 * k + 5]) << 16);
-          st.w = (unsigned)f2bf(v[8 * k + 6]) | ((unsigned)f2bf(v[8 * k + 7]) << 16);
+          st.x = (unsigned)A::from_f(v[8 * k + 0]) | ((unsigned)A::from_f(v[8 * k + 1]) << 16);
+          st.y = (unsigned)A::from_f(v[8 * k + 2]) | ((unsigned)A::from_f(v[8 * k + 3]) << 16);
+          st.z = (unsigned)A::from_f(v[8 * k + 4]) | ((unsigned)A::from_f(v[8 * k + 5]) << 16);
+          st.w = (unsigned)A::from_f(v[8 * k + 6]) | ((unsigned)A::from_f(v[8 * k + 7]) << 16);
           *reinterpret_cast<uint4*>(out + pix * 32 + half * 16 + 8 * k) = st;
         }
       }
@@ -423,54 +454,52 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
     if (j + 1 < nsteps) fetch(d0 + j);  // plane of step j + 1
     const bool v0 = j < nd, v1 = j >= 1 && j - 1 < nd, v2 = j >= 2;
 #if SFM_CONV_EXP == 3  // timing experiment: operands read once per plane, not per group (wrong results)
-    bf16x8 wf[3][3], xf[4];
+    v8 wf[3][3], xf[4];
 #pragma unroll
     for (int dz = 0; dz < 3; ++dz)
 #pragma unroll
       for (int dy = 0; dy < 3; ++dy)
-        wf[dz][dy] = *reinterpret_cast<const bf16x8*>(lds_w + (((dz * 3 + dy) * 3) * 32 + r) * 64 + swz(h, r) * 16);
+        wf[dz][dy] = *reinterpret_cast<const v8*>(lds_w + (((dz * 3 + dy) * 3) * 32 + r) * 64 + swz(h, r) * 16);
 #pragma unroll
     for (int ir = 0; ir < 4; ++ir)
-      xf[ir] = *reinterpret_cast<const bf16x8*>(lds_in + ((wrow + ir) * kHaloX + wcol + r) * 64 + swz(h, wcol + r) * 16);
+      xf[ir] = *reinterpret_cast<const v8*>(lds_in + ((wrow + ir) * kHaloX + wcol + r) * 64 + swz(h, wcol + r) * 16);
 #endif
 #pragma unroll
     for (int g = 0; g < 6; ++g) {
 #if SFM_CONV_EXP != 3
       const int kb = g / 3, dx = g - 3 * (g / 3);
       const int c = kb * 2 + h;
-      bf16x8 wf[3][3], xf[4];
+      v8 wf[3][3], xf[4];
 #pragma unroll
       for (int dz = 0; dz < 3; ++dz)
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
-          wf[dz][dy] = *reinterpret_cast<const bf16x8*>(lds_w + (((dz * 3 + dy) * 3 + dx) * 32 + r) * 64 + swz(c, r) * 16);
+          wf[dz][dy] = *reinterpret_cast<const v8*>(lds_w + (((dz * 3 + dy) * 3 + dx) * 32 + r) * 64 + swz(c, r) * 16);
       const int p = wcol + r + dx;
 #pragma unroll
       for (int ir = 0; ir < 4; ++ir)
-        xf[ir] = *reinterpret_cast<const bf16x8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
+        xf[ir] = *reinterpret_cast<const v8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
 #endif
       if (v0) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
           for (int o = 0; o < 2; ++o)
-            acc[PH][o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[0][dy], xf[o + dy], acc[PH][o], 0, 0, 0);
+            acc[PH][o] = A::mfma(wf[0][dy], xf[o + dy], acc[PH][o]);
       }
       if (v1) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
           for (int o = 0; o < 2; ++o)
-            acc[(PH + 2) % 3][o] =
-                __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[1][dy], xf[o + dy], acc[(PH + 2) % 3][o], 0, 0, 0);
+            acc[(PH + 2) % 3][o] = A::mfma(wf[1][dy], xf[o + dy], acc[(PH + 2) % 3][o]);
       }
       if (v2) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
           for (int o = 0; o < 2; ++o)
-            acc[(PH + 1) % 3][o] =
-                __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[2][dy], xf[o + dy], acc[(PH + 1) % 3][o], 0, 0, 0);
+            acc[(PH + 1) % 3][o] = A::mfma(wf[2][dy], xf[o + dy], acc[(PH + 1) % 3][o]);
       }
     }
     if (v2) {  // output plane m = j - 2 is complete
@@ -492,7 +521,7 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
 
 // [B][C][P] (fp32 or bf16) -> [B][P][C] bf16, P = D*H*W.  A 64-pixel x C tile
 // through LDS: coalesced reads along P per channel, coalesced 16-byte writes.
-template <typename T>
+template <typename T, bool F16>
 __global__ __launch_bounds__(256) void k_to_channels_last(const T* __restrict__ in, int C, int64_t P,
                                                           unsigned short* __restrict__ out) {
   __shared__ float tile[64][65];
@@ -518,7 +547,7 @@ __global__ __launch_bounds__(256) void k_to_channels_last(const T* __restrict__ 
       const int64_t p = p0 + px;
       if (p >= P) continue;
       unsigned short s[8];
-      for (int j = 0; j < 8; ++j) s[j] = f2bf(tile[g * 8 + j][px]);
+      for (int j = 0; j < 8; ++j) s[j] = Act<F16>::from_f(tile[g * 8 + j][px]);
       uint4 v;
       v.x = s[0] | ((unsigned)s[1] << 16);
       v.y = s[2] | ((unsigned)s[3] << 16);
@@ -534,6 +563,7 @@ __global__ __launch_bounds__(256) void k_to_channels_last(const T* __restrict__ 
 // 1 KB contiguous per channel row; values are rounded to bf16 on the way into
 // a [C][256 + 8] LDS tile; each thread then gathers 8 channels of one pixel
 // and writes 16 contiguous bytes.
+template <bool F16>
 __global__ __launch_bounds__(256) void k_to_channels_last_f4(const float* __restrict__ in, int C, int64_t P,
                                                              unsigned short* __restrict__ out) {
   __shared__ unsigned short tile[64][256 + 8];
@@ -546,10 +576,10 @@ __global__ __launch_bounds__(256) void k_to_channels_last_f4(const float* __rest
     float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (p < P) v = *reinterpret_cast<const float4*>(in + ((int64_t)b * C + c) * P + p);  // P % 4 == 0: all 4 valid
     unsigned short* t = &tile[c][4 * q];
-    t[0] = f2bf(v.x);
-    t[1] = f2bf(v.y);
-    t[2] = f2bf(v.z);
-    t[3] = f2bf(v.w);
+    t[0] = Act<F16>::from_f(v.x);
+    t[1] = Act<F16>::from_f(v.y);
+    t[2] = Act<F16>::from_f(v.z);
+    t[3] = Act<F16>::from_f(v.w);
   }
   __syncthreads();
   const int ng = C / 8;
@@ -747,9 +777,12 @@ using namespace sfm;
 
 extern "C" {
 
-int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, const void* weights,
-                   const float* scale, const float* bias, const void* residual, int relu, int cout, void* out,
-                   void* stream) {
+}  // extern "C"
+
+template <bool F16>
+static int conv3_lp(const void* in, int batch, int cin, int depth, int h, int w, const void* weights,
+                    const float* scale, const float* bias, const void* residual, int relu, int cout, void* out,
+                    void* stream) {
   SFM_REQUIRE(in && weights && scale && bias && out, "null pointer argument");
   SFM_REQUIRE(cin == 32 || cin == 64, "cin must be 32 or 64");
   SFM_REQUIRE(cout == 32 || cout == 1, "cout must be 32 or 1");
@@ -759,12 +792,12 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
   SFM_REQUIRE(in != out && (residual == nullptr || residual != out), "conv output must not alias its inputs");
   SFM_REQUIRE(((uintptr_t)in & 15) == 0 && ((uintptr_t)weights & 15) == 0, "conv operands must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
-  ProfScope ps("conv3", s);
+  ProfScope ps(F16 ? "conv3_f16" : "conv3", s);
   const int ntx = (w + kTileX - 1) / kTileX;
   if (cin == 32 && tuning().conv_rolling) {
     // > 64 KB of dynamic LDS must be opted into; set on every launch (cheap,
     // and correct for whichever device is current and from any host thread)
-    SFM_HIP(hipFuncSetAttribute((const void*)k_conv3r, hipFuncAttributeMaxDynamicSharedMemorySize, kRLds));
+    SFM_HIP(hipFuncSetAttribute((const void*)k_conv3r<F16>, hipFuncAttributeMaxDynamicSharedMemorySize, kRLds));
     // Longest plane run that still gives ~one full round of 2 blocks per CU
     // (fewer halo planes and weight stagings per output plane; measured at
     // C2: 8 -> 16 -> 32 planes = 748 -> 772 -> 798 TFLOP/s).
@@ -780,7 +813,7 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
     const int64_t nblk = (int64_t)ntx * nty * ndc * batch;
     SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
     const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
-    hipLaunchKernelGGL(k_conv3r, dim3((unsigned)(per_xcd * kXcds)), dim3(256), kRLds, s, (const unsigned short*)in,
+    hipLaunchKernelGGL(k_conv3r<F16>, dim3((unsigned)(per_xcd * kXcds)), dim3(256), kRLds, s, (const unsigned short*)in,
                        (const unsigned short*)weights, scale, bias, (const unsigned short*)residual, relu,
                        cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w,
                        ntx, nty, ndc, nplanes, (int)nblk, per_xcd);
@@ -789,7 +822,7 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
     const int64_t nblk = (int64_t)ntx * nty * batch * depth;
     SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
     const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
-    hipLaunchKernelGGL(k_conv3, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, (const unsigned short*)in,
+    hipLaunchKernelGGL(k_conv3<F16>, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, (const unsigned short*)in,
                        cin, (const unsigned short*)weights, scale, bias, (const unsigned short*)residual, relu,
                        cout == 32 ? (unsigned short*)out : nullptr, cout == 1 ? (float*)out : nullptr, depth, h, w,
                        ntx, nty, (int)nblk, per_xcd);
@@ -798,8 +831,25 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
   return SFM_OK;
 }
 
-int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
-                              void* stream) {
+extern "C" {
+
+int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, const void* weights,
+                   const float* scale, const float* bias, const void* residual, int relu, int cout, void* out,
+                   void* stream) {
+  return conv3_lp<false>(in, batch, cin, depth, h, w, weights, scale, bias, residual, relu, cout, out, stream);
+}
+
+int sfm_conv3_f16(const void* in, int batch, int cin, int depth, int h, int w, const void* weights,
+                  const float* scale, const float* bias, const void* residual, int relu, int cout, void* out,
+                  void* stream) {
+  return conv3_lp<true>(in, batch, cin, depth, h, w, weights, scale, bias, residual, relu, cout, out, stream);
+}
+
+}  // extern "C"
+
+template <bool F16>
+static int to_channels_last_lp(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
+                               void* stream) {
   SFM_REQUIRE(in && out, "null pointer argument");
   SFM_REQUIRE(in_dtype == 0 || in_dtype == 1, "in_dtype must be 0 (float32) or 1 (bfloat16)");
   SFM_REQUIRE(batch >= 1 && batch <= 65535 && channels >= 8 && channels % 8 == 0 && plane >= 1,
@@ -809,16 +859,28 @@ int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int chann
   ProfScope ps("to_channels_last", s);
   dim3 grid((unsigned)((plane + 63) / 64), batch);
   if (in_dtype == 0 && plane % 4 == 0 && channels <= 64 && ((uintptr_t)in & 15) == 0)
-    hipLaunchKernelGGL(k_to_channels_last_f4, dim3((unsigned)((plane + 255) / 256), batch), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_to_channels_last_f4<F16>, dim3((unsigned)((plane + 255) / 256), batch), dim3(256), 0, s,
                        (const float*)in, channels, plane, (unsigned short*)out);
   else if (in_dtype == 0)
-    hipLaunchKernelGGL(k_to_channels_last<float>, grid, dim3(256), 0, s, (const float*)in, channels, plane,
+    hipLaunchKernelGGL((k_to_channels_last<float, F16>), grid, dim3(256), 0, s, (const float*)in, channels, plane,
                        (unsigned short*)out);
   else
-    hipLaunchKernelGGL(k_to_channels_last<unsigned short>, grid, dim3(256), 0, s, (const unsigned short*)in, channels,
+    hipLaunchKernelGGL((k_to_channels_last<unsigned short, F16>), grid, dim3(256), 0, s, (const unsigned short*)in, channels,
                        plane, (unsigned short*)out);
   SFM_LAUNCHED();
   return SFM_OK;
+}
+
+extern "C" {
+
+int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
+                              void* stream) {
+  return to_channels_last_lp<false>(in, in_dtype, batch, channels, plane, out, stream);
+}
+
+int sfm_to_channels_last_f16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
+                             void* stream) {
+  return to_channels_last_lp<true>(in, in_dtype, batch, channels, plane, out, stream);
 }
 
 int sfm_conv3_f32(const float* in, int batch, int cin, int depth, int h, int w, const float* weights,

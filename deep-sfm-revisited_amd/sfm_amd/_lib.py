@@ -91,6 +91,11 @@ _SIGS = [
       ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
     ("sfm_to_channels_last_bf16", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp]),
+    ("sfm_conv3_f16", ctypes.c_int,
+     [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,
+      ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
+    ("sfm_to_channels_last_f16", ctypes.c_int,
+     [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp]),
     ("sfm_conv3_f32", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,
       ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),

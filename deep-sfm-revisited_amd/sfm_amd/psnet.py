@@ -109,13 +109,14 @@ class PSNet(CostRegularization):
 
     ``feature_fn`` replaces the feature CNN (any callable image -> [B, 32,
     H/4, W/4]); ``conv_precision`` selects the regularisation arithmetic
-    (CostRegularization): "fp32" (default) is the reference's own precision
-    (PSNet.py:159-165 in float32; its MIXED_PREC autocast would run fp16, whose
-    mantissa is still wider than bf16's), "bf16" the faster opt-in path;
+    (CostRegularization): "auto" (default) follows the reference --
+    PSNet.py:159-165 in float32, or in float16 under cfg.MIXED_PREC, the
+    autocast SFMnet.py:164 wraps the depth estimator in (cfgs/kitti.yml:10) --
+    so it resolves to "fp32" or "fp16"; "bf16" is the fastest opt-in path;
     ``cost_dtype`` the sweep volume's storage."""
 
     def __init__(self, nlabel, mindepth=None, cfg=None, feature_fn=None, cost_dtype=torch.float32,
-                 conv_precision="fp32"):
+                 conv_precision="auto"):
         super().__init__(64)
         c = _default_cfg if cfg is None else cfg
         if c.get("COST_BY_COLOR", False) or c.get("COST_BY_COLOR_WITH_FEAT", False):
@@ -124,6 +125,10 @@ class PSNet(CostRegularization):
         self.nlabel = int(nlabel)
         self.mindepth = float(c.MIN_DEPTH)            # the reference reads cfg.MIN_DEPTH too (PSNet.py:44)
         self.cost_dtype = cost_dtype
+        if conv_precision == "auto":
+            conv_precision = "fp16" if c.get("MIXED_PREC", False) else "fp32"
+        if conv_precision not in ("fp32", "fp16", "bf16"):
+            raise ValueError(f"unknown conv precision {conv_precision!r}")
         self.conv_precision = conv_precision
         self.feature_extraction = FeatureExtraction() if feature_fn is None else feature_fn
         if c.get("IND_CONTEXT", False):

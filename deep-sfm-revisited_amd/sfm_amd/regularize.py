@@ -10,9 +10,12 @@ its application at PSNet.py:159-165:
 
 ``CostRegularization.forward`` runs the 12 Conv3d layers as
 ``sfm_conv3_f32`` launches (default ``precision="fp32"``: fp32 activations
-and weights on the f32 matrix cores, the reference's precision) or, with
-``precision="bf16"``, as ``sfm_conv3_bf16`` launches (bf16 channels-last
-activations, fp32 accumulation; the fast opt-in option).  BatchNorm3d is folded in eval mode, ReLU
+and weights on the f32 matrix cores, the reference's precision), with
+``precision="fp16"`` as ``sfm_conv3_f16`` launches (float16 channels-last
+activations and weights, fp32 accumulation: the precision of the reference's
+Conv3d layers under ``cfg.MIXED_PREC`` autocast, SFMnet.py:164) or, with
+``precision="bf16"``, as ``sfm_conv3_bf16`` launches (the fastest opt-in,
+8-bit mantissa).  BatchNorm3d is folded in eval mode, ReLU
 and residual are fused into the epilogue.  There is no PyTorch fallback: without libsfm_hip.so or a GPU
 the call raises.
 """
@@ -26,6 +29,9 @@ from .depth import depth_head
 from .sweep import plane_sweep_cost, quarter_intrinsics
 
 
+_ACT_DTYPE = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+
+
 def convbn_3d(in_planes, out_planes, kernel_size=3, stride=1, pad=1):
     """models/submodule.py:17-20."""
     return nn.Sequential(nn.Conv3d(in_planes, out_planes, kernel_size=kernel_size, padding=pad, stride=stride,
@@ -33,18 +39,49 @@ def convbn_3d(in_planes, out_planes, kernel_size=3, stride=1, pad=1):
                          nn.BatchNorm3d(out_planes))
 
 
-def to_channels_last(cost):
-    """[B, C, L, h, w] fp32/bf16 (device) -> [B, L, h, w, C] bf16 (round to nearest even)."""
+_LP_NAME = {torch.bfloat16: "bf16", torch.float16: "f16"}
+
+
+def to_channels_last(cost, dtype=torch.bfloat16):
+    """[B, C, L, h, w] fp32/bf16 (device) -> [B, L, h, w, C] ``dtype`` (bf16 or
+    fp16, round to nearest even)."""
     if not (isinstance(cost, torch.Tensor) and cost.is_cuda) or cost.dtype not in (torch.float32, torch.bfloat16):
         raise RuntimeError("to_channels_last needs a float32 / bfloat16 device tensor")
+    if dtype not in _LP_NAME:
+        raise RuntimeError("to_channels_last writes bfloat16 or float16")
     cost = cost.contiguous()
     B, C = cost.shape[:2]
     P = cost[0, 0].numel()
-    out = torch.empty((B,) + tuple(cost.shape[2:]) + (C,), dtype=torch.bfloat16, device=cost.device)
+    out = torch.empty((B,) + tuple(cost.shape[2:]) + (C,), dtype=dtype, device=cost.device)
+    fn = "sfm_to_channels_last_" + _LP_NAME[dtype]
     with torch.cuda.device(cost.device):
-        _lib.check(_lib.load().sfm_to_channels_last_bf16(_lib.ptr(cost), 0 if cost.dtype == torch.float32 else 1,
-                                                         B, C, P, _lib.ptr(out), _lib.stream_ptr(cost.device)),
-                   "sfm_to_channels_last_bf16")
+        _lib.check(getattr(_lib.load(), fn)(_lib.ptr(cost), 0 if cost.dtype == torch.float32 else 1,
+                                            B, C, P, _lib.ptr(out), _lib.stream_ptr(cost.device)), fn)
+    return out
+
+
+def _conv3_lp(x, weights, scale, bias, residual, relu, cout, dtype):
+    name = {torch.bfloat16: "bfloat16", torch.float16: "float16"}[dtype]
+    for t, n in ((x, "x"), (weights, "weights")):
+        if not (t.is_cuda and t.dtype == dtype and t.is_contiguous()):
+            raise RuntimeError(f"{n} must be a contiguous {name} device tensor")
+    B, L, h, w, cin = x.shape
+    if tuple(weights.shape) != (27, 32, cin):
+        raise RuntimeError(f"weights must be [27, 32, {cin}]")
+    if residual is not None and (residual.dtype != dtype or tuple(residual.shape) != (B, L, h, w, 32)):
+        raise RuntimeError(f"residual must be {name} [B, L, h, w, 32]")
+    if cout == 32:
+        out = torch.empty((B, L, h, w, 32), dtype=dtype, device=x.device)
+    else:
+        out = torch.empty((B, L, h, w), dtype=torch.float32, device=x.device)
+    scale = scale.to(device=x.device, dtype=torch.float32).contiguous()
+    bias = bias.to(device=x.device, dtype=torch.float32).contiguous()
+    fn = "sfm_conv3_" + _LP_NAME[dtype]
+    with torch.cuda.device(x.device):
+        rc = getattr(_lib.load(), fn)(_lib.ptr(x), B, cin, L, h, w, _lib.ptr(weights), _lib.ptr(scale),
+                                      _lib.ptr(bias), None if residual is None else _lib.ptr(residual.contiguous()),
+                                      1 if relu else 0, cout, _lib.ptr(out), _lib.stream_ptr(x.device))
+        _lib.check(rc, fn)
     return out
 
 
@@ -52,26 +89,13 @@ def conv3_bf16(x, weights, scale, bias, residual=None, relu=False, cout=32):
     """One fused layer: x [B, L, h, w, Cin] bf16, weights [27, 32, Cin] bf16,
     scale/bias [32] fp32 -> [B, L, h, w, 32] bf16 (cout 32) or [B, L, h, w]
     fp32 (cout 1)."""
-    for t, n in ((x, "x"), (weights, "weights")):
-        if not (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous()):
-            raise RuntimeError(f"{n} must be a contiguous bfloat16 device tensor")
-    B, L, h, w, cin = x.shape
-    if tuple(weights.shape) != (27, 32, cin):
-        raise RuntimeError(f"weights must be [27, 32, {cin}]")
-    if residual is not None and (residual.dtype != torch.bfloat16 or tuple(residual.shape) != (B, L, h, w, 32)):
-        raise RuntimeError("residual must be bf16 [B, L, h, w, 32]")
-    if cout == 32:
-        out = torch.empty((B, L, h, w, 32), dtype=torch.bfloat16, device=x.device)
-    else:
-        out = torch.empty((B, L, h, w), dtype=torch.float32, device=x.device)
-    scale = scale.to(device=x.device, dtype=torch.float32).contiguous()
-    bias = bias.to(device=x.device, dtype=torch.float32).contiguous()
-    with torch.cuda.device(x.device):
-        rc = _lib.load().sfm_conv3_bf16(_lib.ptr(x), B, cin, L, h, w, _lib.ptr(weights), _lib.ptr(scale),
-                                        _lib.ptr(bias), None if residual is None else _lib.ptr(residual.contiguous()),
-                                        1 if relu else 0, cout, _lib.ptr(out), _lib.stream_ptr(x.device))
-        _lib.check(rc, "sfm_conv3_bf16")
-    return out
+    return _conv3_lp(x, weights, scale, bias, residual, relu, cout, torch.bfloat16)
+
+
+def conv3_f16(x, weights, scale, bias, residual=None, relu=False, cout=32):
+    """``conv3_bf16`` with float16 activations, weights and residual
+    (sfm_conv3_f16)."""
+    return _conv3_lp(x, weights, scale, bias, residual, relu, cout, torch.float16)
 
 
 class CostRegularization(nn.Module):
@@ -114,12 +138,12 @@ class CostRegularization(nn.Module):
         return (str(device),) + tuple((t.data_ptr(), t._version) for t in list(self.parameters()) + list(self.buffers()))
 
     def pack(self, device, precision="bf16"):
-        """Packed weights [27][32][Cin] (bf16, or fp32 for precision "fp32")
-        and folded fp32 scale/bias per layer."""
+        """Packed weights [27][32][Cin] in the precision's type (fp32 / fp16 /
+        bf16) and folded fp32 scale/bias per layer."""
         key = self._key(device) + (precision,)
         if self._packed is not None and self._packed_key == key:
             return self._packed
-        wdt = torch.float32 if precision == "fp32" else torch.bfloat16
+        wdt = _ACT_DTYPE[precision]
         packed = []
         with torch.no_grad():
             for conv, bn, relu, resid in self.layer_plan():
@@ -146,10 +170,11 @@ class CostRegularization(nn.Module):
     def forward(self, cost, precision="fp32"):
         """cost [B, Cin, L, h, w] fp32 or bf16 (the sweep's volume) -> [B, 1, L, h, w] fp32.
         ``precision``: "fp32" (default: fp32 activations, weights and
-        accumulation, sfm_conv3_f32, the reference's precision) or "bf16" (bf16
-        activations and weights, fp32 accumulation: sfm_conv3_bf16, the fast
-        opt-in)."""
-        if precision not in ("bf16", "fp32"):
+        accumulation, sfm_conv3_f32, the reference's precision), "fp16" (fp16
+        activations and weights, fp32 accumulation: sfm_conv3_f16, the
+        reference's precision under cfg.MIXED_PREC) or "bf16" (bf16, fp32
+        accumulation: sfm_conv3_bf16, the fastest opt-in)."""
+        if precision not in _ACT_DTYPE:
             raise ValueError(f"unknown conv precision {precision!r}")
         if not (isinstance(cost, torch.Tensor) and cost.is_cuda):
             raise RuntimeError("CostRegularization.forward needs a device tensor (HIP path, no CPU fallback)")
@@ -162,10 +187,10 @@ class CostRegularization(nn.Module):
             raise RuntimeError(f"cost has {C} channels, the first layer expects {packed[0]['cin']}")
         lib = _lib.load()
         dev = cost.device
-        fp32 = precision == "fp32"
-        adt = torch.float32 if fp32 else torch.bfloat16
-        to_cl = lib.sfm_to_channels_last_f32 if fp32 else lib.sfm_to_channels_last_bf16
-        conv = lib.sfm_conv3_f32 if fp32 else lib.sfm_conv3_bf16
+        adt = _ACT_DTYPE[precision]
+        suffix = {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}[precision]
+        to_cl = getattr(lib, "sfm_to_channels_last_" + suffix)
+        conv = getattr(lib, "sfm_conv3_" + suffix)
         with torch.cuda.device(dev):
             stream = _lib.stream_ptr(dev)
             x = torch.empty((B, L, h, w, C), dtype=adt, device=dev)
@@ -183,7 +208,7 @@ class CostRegularization(nn.Module):
                 rc = conv(_lib.ptr(cur), B, lay["cin"], L, h, w, _lib.ptr(lay["w"]), _lib.ptr(lay["scale"]),
                           _lib.ptr(lay["bias"]), None if res is None else _lib.ptr(res), 1 if lay["relu"] else 0,
                           lay["cout"], _lib.ptr(dst), stream)
-                _lib.check(rc, "sfm_conv3_f32" if fp32 else "sfm_conv3_bf16")
+                _lib.check(rc, "sfm_conv3_" + suffix)
                 # cost0 after dres0 (layer 1) and after every residual add is the next block's input
                 if li == 1 or lay["resid"]:
                     keep = dst

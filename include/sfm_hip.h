@@ -344,6 +344,21 @@ int sfm_conv3_bf16(const void* in, int batch, int cin, int depth, int h, int w, 
 int sfm_to_channels_last_bf16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
                               void* stream);
 
+/* The same layer with float16 activations and weights (11-bit mantissa,
+ * fp32 accumulation on v_mfma_f32_32x32x16_f16): the precision the
+ * reference's Conv3d layers run at under cfg.MIXED_PREC autocast
+ * (models/SFMnet.py:164, cfgs/kitti.yml:10).  Arguments and layouts as
+ * sfm_conv3_bf16, every 16-bit operand IEEE half. */
+int sfm_conv3_f16(const void* in, int batch, int cin, int depth, int h, int w, const void* weights,
+                  const float* scale, const float* bias, const void* residual, int relu, int cout, void* out,
+                  void* stream);
+
+/* [batch][channels][plane] float32 (in_dtype 0) or bfloat16 (1) ->
+ * [batch][plane][channels] float16 (round to nearest even), sfm_conv3_f16's
+ * layout. */
+int sfm_to_channels_last_f16(const void* in, int in_dtype, int batch, int channels, int64_t plane, void* out,
+                             void* stream);
+
 /* The same layer at the reference's precision (conv_precision "fp32"):
  * float32 operands on v_mfma_f32_32x32x2_f32 (an exact fmaf chain: products
  * and sums round as float32 arithmetic; only the summation order differs from

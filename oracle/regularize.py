@@ -10,6 +10,9 @@ evaluated with BatchNorm in eval mode (running statistics).
   only by summation order (and the rare bf16 rounding flip it causes), so
   tests compare against it tightly and against ``regularize_fp32`` with the
   bf16 storage tolerance.
+* ``regularize_f16``   — the same with float16 storage (``sfm_conv3_f16``;
+  the precision of the reference's Conv3d layers under cfg.MIXED_PREC
+  autocast, models/SFMnet.py:164).
 
 Parity unpinned by the reference: it holds no fixtures for this stack; the
 oracle is the reference's own module code run in fp32 (the nn.Conv3d /
@@ -22,6 +25,10 @@ import torch.nn.functional as F
 
 def _bf16(t):
     return t.to(torch.bfloat16).to(torch.float32)
+
+
+def _f16(t):
+    return t.to(torch.float16).to(torch.float32)
 
 
 def _conv_bn(x, conv, bn, wrnd=lambda t: t):
@@ -78,3 +85,8 @@ def regularize_fp32_plan(mod, cost):
 def regularize_bf16(mod, cost):
     with torch.no_grad():
         return _run(mod, cost, _bf16)
+
+
+def regularize_f16(mod, cost):
+    with torch.no_grad():
+        return _run(mod, cost, _f16)

@@ -472,3 +472,124 @@ def test_default_psnet_module_vs_float64_reference(cuda, golden):
     r16 = _rel(d16.cpu(), want)
     print(dict(fp32_max=float(r1.max()), bf16_median=float(r16.median()), bf16_max=float(r16.max())))
     assert float(r16.max()) > float(r1.max())
+
+
+# ---------------------------------------------------------------------------
+# float16 stack (sfm_conv3_f16): the precision of the reference's Conv3d
+# layers under cfg.MIXED_PREC autocast (SFMnet.py:164, cfgs/kitti.yml:10).
+# Same kernels as bf16, f16 MFMA and conversions: one layer within half an
+# f16 ulp (2^-11 relative) of the fp32 conv of the same f16 operands; the
+# rolling and per-plane kernels bit-identical; the stack close to the
+# f16-storage oracle and to fp32; the depth against the float64 reference.
+
+def _f16_ulp_close(got, want):
+    tol = 2.0 ** -11 * want.abs() * 1.001 + 1e-5
+    bad = (got - want).abs() > tol
+    return int(bad.sum()), float((got - want).abs().max())
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 5, 7, 13), (1, 64, 2, 16, 16)])
+def test_channels_last_f16_exact(cuda, shape):
+    from sfm_amd.regularize import to_channels_last
+    x = torch.randn(*shape, generator=torch.Generator().manual_seed(2)) * 10
+    got = to_channels_last(x.to(cuda), torch.float16).cpu()
+    want = x.permute(0, 2, 3, 4, 1).to(torch.float16)
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+
+
+@pytest.mark.parametrize("B,cin,D,h,w,relu,resid,cout", [
+    (1, 32, 3, 4, 64, False, False, 32),
+    (2, 64, 5, 7, 70, True, False, 32),
+    (1, 32, 4, 9, 131, False, True, 32),
+    (1, 32, 6, 5, 33, False, False, 1),
+])
+def test_conv_layer_f16(cuda, B, cin, D, h, w, relu, resid, cout):
+    from sfm_amd.regularize import conv3_f16
+    g = torch.Generator().manual_seed(B * 100 + cin + D + h + w + 1)
+    x = torch.randn(B, cin, D, h, w, generator=g).to(torch.float16).float()
+    wt = (torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1).to(torch.float16).float()
+    scale = 0.5 + torch.rand(cout, generator=g)
+    bias = 0.3 * torch.randn(cout, generator=g)
+    res = torch.randn(B, 32, D, h, w, generator=g).to(torch.float16).float() if resid else None
+    want = F.conv3d(x.double(), wt.double(), None, 1, 1) * scale.double().view(1, -1, 1, 1, 1) \
+        + bias.double().view(1, -1, 1, 1, 1)
+    if relu:
+        want = torch.relu(want)
+    if res is not None:
+        want = want + res.double()
+    want = want.float()
+    wp = torch.zeros(27, 32, cin)
+    wp[:, :cout] = wt.permute(2, 3, 4, 0, 1).reshape(27, cout, cin)
+    sc, bi = torch.ones(32), torch.zeros(32)
+    sc[:cout], bi[:cout] = scale, bias
+    xcl = x.permute(0, 2, 3, 4, 1).contiguous().to(torch.float16).to(cuda)
+    rcl = None if res is None else res.permute(0, 2, 3, 4, 1).contiguous().to(torch.float16).to(cuda)
+    got = conv3_f16(xcl, wp.to(torch.float16).to(cuda), sc, bi, rcl, relu, cout).cpu()
+    if cout == 32:
+        nbad, mx = _f16_ulp_close(got.float().permute(0, 4, 1, 2, 3), want)
+        assert nbad == 0, (nbad, mx)
+    else:
+        err = (got - want[:, 0]).abs() - (1e-5 * want[:, 0].abs() + 1e-5)
+        assert float(err.max()) <= 0, float((got - want[:, 0]).abs().max())
+
+
+def test_rolling_kernel_equals_per_plane_kernel_f16(cuda):
+    from sfm_amd import _lib
+    from sfm_amd.regularize import conv3_f16
+    g = torch.Generator().manual_seed(9)
+    D, h, w = 13, 9, 70
+    x = torch.randn(1, D, h, w, 32, generator=g).to(torch.float16).to(cuda)
+    wp = (torch.randn(27, 32, 32, generator=g) * 0.1).to(torch.float16).to(cuda)
+    sc, bi = 0.5 + torch.rand(32, generator=g), 0.1 * torch.randn(32, generator=g)
+    res = torch.randn(1, D, h, w, 32, generator=g).to(torch.float16).to(cuda)
+    outs = []
+    try:
+        for rolling in (0, 1):
+            _lib.tune("conv_rolling", rolling)
+            outs.append((conv3_f16(x, wp, sc, bi, res, False, 32).cpu(), conv3_f16(x, wp, sc, bi, None, True, 1).cpu()))
+    finally:
+        _lib.tune("conv_rolling", 1)
+    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16))
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("B,cin,L,h,w", [(1, 64, 16, 12, 20), (1, 32, 7, 5, 67)])
+def test_stack_f16_vs_oracle(cuda, B, cin, L, h, w):
+    """Relative L2 against the f16-storage oracle <= 3e-3 and against fp32 <=
+    5e-3 (bf16's bars are 2e-2 / 3e-2: three more mantissa bits)."""
+    m = _module(11 + L, cin)
+    cost = torch.randn(B, cin, L, h, w, generator=torch.Generator().manual_seed(L))
+    got = m.to(cuda)(cost.to(cuda), precision="fp16").cpu()
+    m = m.cpu()
+    want16 = R.regularize_f16(m, cost)
+    want32 = R.regularize_fp32(m, cost)
+    r16 = float((got - want16).norm() / want16.norm())
+    r32 = float((got - want32).norm() / want32.norm())
+    print(dict(r16=r16, r32=r32))
+    assert r16 <= 3e-3, r16
+    assert r32 <= 5e-3, r32
+
+
+def test_psnet_fp16_depth_vs_float64_reference(cuda, golden):
+    """The fp16 stack (what cfg.MIXED_PREC selects) against the float64
+    reference PSNet depth (psnet64.npz): median <= 2e-3, max <= 2e-2
+    relative (measured 1.2e-3 / 9.9e-3; an 11-bit mantissa cannot meet the
+    fp32 path's 1e-4, and neither can the reference's own fp16 autocast), and
+    five times closer than the bf16 stack at the median (measured 12x:
+    bf16 1.4e-2 / 0.11)."""
+    from sfm_amd.regularize import psnet_depth
+    g, m = _psnet64(golden)
+    inp = g["input"]
+    L, md = int(inp["nlabel"]), float(inp["min_depth"])
+    hw = tuple(int(x) for x in inp["image_hw"])
+    d = lambda k: torch.from_numpy(k).to(cuda)
+    want = torch.from_numpy(g["out64"]["depth"])
+    res = {}
+    for prec in ("fp16", "bf16"):
+        got = psnet_depth(d(inp["ref_fea"]), d(inp["tgt_fea"]), d(inp["pose_rescaled"])[:, 0], d(inp["K"]),
+                          d(inp["Kinv"]), m.to(cuda), L, md, out_hw=hw, precision=prec).cpu()
+        r = _rel(got, want)
+        res[prec] = (float(r.median()), float(r.max()))
+    print(res)
+    assert res["fp16"][0] <= 2e-3 and res["fp16"][1] <= 2e-2, res
+    assert res["fp16"][0] * 5 <= res["bf16"][0], res
