@@ -73,6 +73,24 @@
 #ifndef SFM_MF2_EXP
 #define SFM_MF2_EXP 0
 #endif
+// wave priority around the tile loop's MFMA groups (experiment: 1 raises it
+// for the a / aa / z group so the matrix pipe is fed first, 2 for the sign
+// harvest instead; 0: no s_setprio).  Both measured ~6 % slower: s_setprio
+// is a scheduling barrier and splits the compiler's interleave of the sign
+// harvest between the MFMAs (profiles/r04_mf2_prio_pk_ab.txt)
+#ifndef SFM_MF2_PRIO
+#define SFM_MF2_PRIO 0
+#endif
+#if SFM_MF2_PRIO == 1
+#define MF2_PRIO_HI() __builtin_amdgcn_s_setprio(1)
+#define MF2_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#elif SFM_MF2_PRIO == 2
+#define MF2_PRIO_HI() __builtin_amdgcn_s_setprio(0)
+#define MF2_PRIO_LO() __builtin_amdgcn_s_setprio(1)
+#else
+#define MF2_PRIO_HI() ((void)0)
+#define MF2_PRIO_LO() ((void)0)
+#endif
 // the tile loop's fragment addresses from one lane base per two tiles (1;
 // measured 0.8 % slower than the lane id per tile, 0: profiles/r04_mf2_ln1_ab.txt)
 #ifndef SFM_MF2_LN1
@@ -590,11 +608,15 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #else
 #define MF2_LN mf2_lane()
 #endif
+            MF2_PRIO_HI();
             aA = mf2_a(mf2_load_ab(fr + (size_t)(t + 1) * kTileHalves, MF2_LN), A1, A2);
             zB = mf2_z(mf2_load_d(fr + (size_t)t * kTileHalves, MF2_LN), NL, NH, aB);
+            MF2_PRIO_LO();
             mf2_signs(zA, s1, s2);
+            MF2_PRIO_HI();
             aB = mf2_a(mf2_load_ab(fr + (size_t)(t + 2) * kTileHalves, MF2_LN), A1, A2);
             zA = mf2_z(mf2_load_d(fr + (size_t)(t + 1) * kTileHalves, MF2_LN), NL, NH, aA);
+            MF2_PRIO_LO();
             mf2_signs(zB, s1, s2);
 #undef MF2_LN
           }

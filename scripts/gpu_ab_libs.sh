@@ -7,7 +7,7 @@
 set -u
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1
-lib() { if [ "$1" = prod ]; then echo deep-sfm-revisited_amd/sfm_amd/libsfm_hip.so; else echo scripts/exp/libsfm_hip_$1.so; fi; }
+lib() { if [ "$1" = prod ]; then echo deep-sfm-revisited_amd/sfm_amd/libsfm_hip.so; else echo ${EXPDIR:-scripts/exp}/libsfm_hip_$1.so; fi; }
 for r in $(seq 1 ${ROUNDS:-2}); do
   for L in ${LIBS}; do
     echo "== round $r lib $L"
