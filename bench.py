@@ -359,8 +359,18 @@ def regularize_roofline(cost, steps=3, precision="bf16"):
 
 def rank_device_index(local):
     """The GPU a rank drives: its LOCAL_RANK (one process per GPU of the node;
-    dist.init binds the RCCL communicator to the same index)."""
-    return int(local)
+    dist.init binds the RCCL communicator to the same index).  Under
+    SFM_BENCH_SHARED_GPU=1 (a rehearsal of the N-rank path on a one-GPU box,
+    never a measurement) every rank drives device 0."""
+    return 0 if _shared_gpu() else int(local)
+
+
+def _shared_gpu():
+    """SFM_BENCH_SHARED_GPU=1: every rank on device 0 over gloo -- the real
+    GPU step, rank sharding, barrier, max-over-ranks timing and gather run
+    with N ranks on a one-GPU box (tests/test_gpu_bench_ranks.py).  The line
+    is marked "rehearsal" and its value is not a multi-GPU measurement."""
+    return os.environ.get("SFM_BENCH_SHARED_GPU") == "1"
 
 
 def _stub_mode():
@@ -425,7 +435,7 @@ def _main_gpu(args, dist):
     import torch
     from sfm_amd import _lib, ransac, synth
     from sfm_amd.pipeline import TwoViewHotPath
-    rank, world, local = dist.init()
+    rank, world, local = dist.init(backend="gloo" if _shared_gpu() else None)
     dev = torch.device("cuda", rank_device_index(local))
     torch.cuda.set_device(dev)
     B = args.batch
@@ -521,6 +531,8 @@ def _main_gpu(args, dist):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
+            **({"rehearsal": f"{world} ranks share one GPU over gloo (SFM_BENCH_SHARED_GPU): not a "
+                              f"multi-GPU measurement"} if _shared_gpu() else {}),
             "src_hash": src_hash(),
             "dtype": "f64+" + ("f32" if s == 4 else "bf16"),
             "data": (f"synthetic (seeded {hwtxt.split()[0]}-shaped rigid scene, 0.5 px noise, 15% outlier flow, "

@@ -47,6 +47,8 @@ def gather_rows(t, world):
     returns the concatenation in rank order (every rank receives it)."""
     if world == 1 or not dist.is_initialized():
         return t
+    if t.is_cuda and dist.get_backend() == "gloo":      # gloo gathers host tensors only
+        return gather_rows(t.cpu(), world).to(t.device)
     n = torch.tensor([t.shape[0]], device=t.device, dtype=torch.int64)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n)
@@ -62,6 +64,8 @@ def reduce_max(value, device=None):
     """Max of a Python float over ranks (timing: the slowest rank defines the step)."""
     if not dist.is_initialized():
         return float(value)
+    if dist.get_backend() == "gloo":
+        device = None
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
