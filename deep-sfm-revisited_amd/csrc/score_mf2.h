@@ -257,6 +257,35 @@ __device__ __forceinline__ void mf2_signs(const MfZ& r, uint32_t (&s1)[16], uint
   }
 }
 constexpr bool kMf2Fold = SFM_MF2_FOLD;
+
+// SFM_MF2_PB: the sign harvest as one v_perm_b32 + one v_bitop3_b32 per
+// register and tile instead of two v_alignbit_b32: perm replicates sign(z1)
+// into the low 16 bits and sign(z2) into the high 16 (selector bytes 9 / 11 =
+// bit 31 of src1 / src0), bitop3 ORs the tile's bit of each half into the
+// string (s | (x & m), m = 0x00010001 << (t & 15)); tiles 0..15 go to one
+// string register, 16..31 to another, and two perms per register rebuild s1 /
+// s2 with bit t = tile t after the loop.  Timing experiment: the same
+// instruction count with cheaper op types measured 0.5 % slower -- the loop is
+// bound by VALU instructions per tile, not their type
+// (profiles/r04_mf2_prio_pk_ab.txt).
+#ifndef SFM_MF2_PB
+#define SFM_MF2_PB 0
+#endif
+__device__ __forceinline__ void mf2_signs_pb(const MfZ& r, uint32_t (&sv)[16], uint32_t m) {
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const uint32_t x = __builtin_amdgcn_perm(__float_as_uint(r.z2[g]), __float_as_uint(r.z1[g]), 0x0B0B0909u);
+    sv[g] = __builtin_amdgcn_bitop3_b32(sv[g], x, m, 0xF8);      // sv | (x & m)
+  }
+}
+// queue entry (candidate row << 24 | span-relative point) of string bit j:
+// bit j = tile kMf2Tiles - 1 - j (alignbit strings) or tile j (SFM_MF2_PB)
+__device__ __forceinline__ uint32_t mf2_qbase(int g, int hl, int rl) {
+  return ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)((SFM_MF2_PB ? 0 : 32 * (kMf2Tiles - 1)) + rl);
+}
+__device__ __forceinline__ uint32_t mf2_qentry(uint32_t base, uint32_t uu) {
+  return SFM_MF2_PB ? base + 32u * (uint32_t)__builtin_ctz(uu) : base - 32u * (uint32_t)__builtin_ctz(uu);
+}
 // undecided evaluations of a decision-string pair
 __device__ __forceinline__ uint32_t mf2_undecided(uint32_t s1, uint32_t s2) {
   return kMf2Fold ? (s2 & ~s1) : ~(s1 | s2);
@@ -598,6 +627,34 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           MfZ zA, zB;
           aB = mf2_a(mf2_load_ab(fr + (size_t)1 * kTileHalves, mf2_lane()), A1, A2);
           zA = mf2_z(mf2_load_d(fr, mf2_lane()), NL, NH, aA);
+#if SFM_MF2_PB
+          static_assert(kMf2Tiles == 32, "two 16-tile halves");
+          // s1 / s2 hold tiles 0..15 / 16..31 (both signs each) until the end
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            uint32_t (&sv)[16] = h2 ? s2 : s1;
+#pragma unroll 1
+            for (int t = 16 * h2 + 1; t < 16 * h2 + 16 && t < kMf2Tiles - 1; t += 2) {
+              const uint32_t m = 0x00010001u << ((t - 1) & 15);
+              aA = mf2_a(mf2_load_ab(fr + (size_t)(t + 1) * kTileHalves, mf2_lane()), A1, A2);
+              zB = mf2_z(mf2_load_d(fr + (size_t)t * kTileHalves, mf2_lane()), NL, NH, aB);
+              mf2_signs_pb(zA, sv, m);                                   // tile t - 1
+              aB = mf2_a(mf2_load_ab(fr + (size_t)(t + 2) * kTileHalves, mf2_lane()), A1, A2);
+              zA = mf2_z(mf2_load_d(fr + (size_t)(t + 1) * kTileHalves, mf2_lane()), NL, NH, aA);
+              mf2_signs_pb(zB, sv, m << 1);                              // tile t
+            }
+          }
+          zB = mf2_z(mf2_load_d(fr + (size_t)(kMf2Tiles - 1) * kTileHalves, mf2_lane()), NL, NH, aB);
+          mf2_signs_pb(zA, s2, 0x00010001u << 14);                       // tile 30
+          mf2_signs_pb(zB, s2, 0x00010001u << 15);                       // tile 31
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {                                 // bit t = tile t
+            const uint32_t lo = s1[g], hi = s2[g];
+            s1[g] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);          // z1 signs: lo.low16 | hi.low16 << 16
+            s2[g] = __builtin_amdgcn_perm(hi, lo, 0x07060302u);          // z2 signs: lo.high16 | hi.high16 << 16
+          }
+          if (false)
+#endif
 #pragma unroll 1
           for (int t = 1; t < kMf2Tiles - 1; t += 2) {
 #if SFM_MF2_LN1
@@ -620,9 +677,11 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
             mf2_signs(zB, s1, s2);
 #undef MF2_LN
           }
+#if !SFM_MF2_PB
           zB = mf2_z(mf2_load_d(fr + (size_t)(kMf2Tiles - 1) * kTileHalves, mf2_lane()), NL, NH, aB);
           mf2_signs(zA, s1, s2);
           mf2_signs(zB, s1, s2);
+#endif
         } else {
         // two accumulator sets: tile t+1's MFMAs beside tile t's decisions
         // (the last pair peeled, so the loop body has no conditional MFMA)
@@ -680,9 +739,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
             const uint32_t uu = mf2_undecided(s1[g], s2[g]);
-            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+            const uint32_t top = mf2_qbase(g, hl, rl);
             if (uu) {
-              *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
+              *q++ = mf2_qentry(top, uu);
               more |= (uu & (uu - 1u)) ? (1u << g) : 0u;
             }
           }
@@ -692,9 +751,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
               if (more & (1u << g)) {
                 uint32_t uu = mf2_undecided(s1[g], s2[g]);
                 uu &= uu - 1u;
-                const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+                const uint32_t top = mf2_qbase(g, hl, rl);
                 while (uu) {
-                  *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
+                  *q++ = mf2_qentry(top, uu);
                   uu &= uu - 1u;
                 }
               }
@@ -704,9 +763,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
             uint32_t uu = mf2_undecided(s1[g], s2[g]);
-            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+            const uint32_t top = mf2_qbase(g, hl, rl);
             while (uu) {
-              *q++ = top - 32u * (uint32_t)__builtin_ctz(uu);
+              *q++ = mf2_qentry(top, uu);
               uu &= uu - 1u;
             }
           }
@@ -715,9 +774,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
           for (int g = 0; g < 16; ++g) {
             uint32_t uu = mf2_undecided(s1[g], s2[g]);
-            const uint32_t top = ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
+            const uint32_t top = mf2_qbase(g, hl, rl);
             while (uu) {
-              if (pos >= 0 && pos < kMf2Queue) queue[pos] = top - 32u * (uint32_t)__builtin_ctz(uu);
+              if (pos >= 0 && pos < kMf2Queue) queue[pos] = mf2_qentry(top, uu);
               uu &= uu - 1u;
               ++pos;
             }
