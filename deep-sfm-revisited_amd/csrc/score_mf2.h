@@ -271,6 +271,9 @@ constexpr bool kMf2Fold = SFM_MF2_FOLD;
 #ifndef SFM_MF2_PB
 #define SFM_MF2_PB 0
 #endif
+#ifndef SFM_MF2_PTR
+#define SFM_MF2_PTR 0
+#endif
 __device__ __forceinline__ void mf2_signs_pb(const MfZ& r, uint32_t (&sv)[16], uint32_t m) {
 #pragma unroll
   for (int g = 0; g < 16; ++g) {
@@ -652,6 +655,27 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
             const uint32_t lo = s1[g], hi = s2[g];
             s1[g] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);          // z1 signs: lo.low16 | hi.low16 << 16
             s2[g] = __builtin_amdgcn_perm(hi, lo, 0x07060302u);          // z2 signs: lo.high16 | hi.high16 << 16
+          }
+          if (false)
+#endif
+#if SFM_MF2_PTR
+          // one lane pointer walking the span: the four fragment loads of
+          // two tiles are immediate offsets from it, one VALU add per two
+          // tiles instead of a lane-id copy + shift-add per load.  Timing
+          // experiment: 97 instead of 104 VALU per two tiles in the loop, but
+          // the pointer costs 18 dwords of spills outside it; measured equal
+          // to 1.3 % slower (profiles/r04_mf2_prio_pk_ab.txt)
+          {
+            const _Float16* pt = fr + mf2_lane() * 8 + kTileHalves;      // tile 1, this lane
+#pragma unroll 1
+            for (int t = 1; t < kMf2Tiles - 1; t += 2, pt += 2 * kTileHalves) {
+              aA = mf2_a(mf2_load_ab(pt + kTileHalves, 0), A1, A2);        // a(t + 1)
+              zB = mf2_z(mf2_load_d(pt, 0), NL, NH, aB);                   // z(t)
+              mf2_signs(zA, s1, s2);                                       // t - 1
+              aB = mf2_a(mf2_load_ab(pt + 2 * kTileHalves, 0), A1, A2);    // a(t + 2)
+              zA = mf2_z(mf2_load_d(pt + kTileHalves, 0), NL, NH, aA);     // z(t + 1)
+              mf2_signs(zB, s1, s2);                                       // t
+            }
           }
           if (false)
 #endif
