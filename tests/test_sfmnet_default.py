@@ -85,3 +85,18 @@ def test_default_depth_precision_is_the_references():
     assert PSNet(16, 1.0, cfg=kitti(), conv_precision="fp32").conv_precision == "fp32"
     with pytest.raises(ValueError):
         PSNet(16, 1.0, conv_precision="fp8")
+
+
+def test_regularisation_precision_is_validated_before_device_work():
+    """CostRegularization.forward names the precisions it knows (fp32 / fp16 /
+    bf16) and refuses others before touching a device; on a host tensor the
+    HIP path refuses to run (no CPU fallback)."""
+    import torch
+    from sfm_amd.regularize import CostRegularization
+    m = CostRegularization(64)
+    x = torch.zeros(1, 64, 2, 3, 4)
+    with pytest.raises(ValueError, match="precision"):
+        m(x, precision="fp8")
+    for prec in ("fp32", "fp16", "bf16"):
+        with pytest.raises(RuntimeError, match="device tensor"):
+            m(x, precision=prec)
