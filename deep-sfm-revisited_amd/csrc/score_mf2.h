@@ -73,24 +73,9 @@
 #ifndef SFM_MF2_EXP
 #define SFM_MF2_EXP 0
 #endif
-// wave priority around the tile loop's MFMA groups (experiment: 1 raises it
-// for the a / aa / z group so the matrix pipe is fed first, 2 for the sign
-// harvest instead; 0: no s_setprio).  Both measured ~6 % slower: s_setprio
-// is a scheduling barrier and splits the compiler's interleave of the sign
-// harvest between the MFMAs (profiles/r04_mf2_prio_pk_ab.txt)
-#ifndef SFM_MF2_PRIO
-#define SFM_MF2_PRIO 0
-#endif
-#if SFM_MF2_PRIO == 1
-#define MF2_PRIO_HI() __builtin_amdgcn_s_setprio(1)
-#define MF2_PRIO_LO() __builtin_amdgcn_s_setprio(0)
-#elif SFM_MF2_PRIO == 2
-#define MF2_PRIO_HI() __builtin_amdgcn_s_setprio(0)
-#define MF2_PRIO_LO() __builtin_amdgcn_s_setprio(1)
-#else
-#define MF2_PRIO_HI() ((void)0)
-#define MF2_PRIO_LO() ((void)0)
-#endif
+// (Round 4 also measured, and dropped: aa as packed v_pk_mul_f32; s_setprio
+// around the MFMA groups; the sign harvest as v_perm_b32 + v_bitop3_b32; a
+// lane pointer walking the span -- profiles/r04_mf2_prio_pk_ab.txt.)
 // the tile loop's fragment addresses from one lane base per two tiles (1;
 // measured 0.8 % slower than the lane id per tile, 0: profiles/r04_mf2_ln1_ab.txt)
 #ifndef SFM_MF2_LN1
@@ -258,36 +243,13 @@ __device__ __forceinline__ void mf2_signs(const MfZ& r, uint32_t (&s1)[16], uint
 }
 constexpr bool kMf2Fold = SFM_MF2_FOLD;
 
-// SFM_MF2_PB: the sign harvest as one v_perm_b32 + one v_bitop3_b32 per
-// register and tile instead of two v_alignbit_b32: perm replicates sign(z1)
-// into the low 16 bits and sign(z2) into the high 16 (selector bytes 9 / 11 =
-// bit 31 of src1 / src0), bitop3 ORs the tile's bit of each half into the
-// string (s | (x & m), m = 0x00010001 << (t & 15)); tiles 0..15 go to one
-// string register, 16..31 to another, and two perms per register rebuild s1 /
-// s2 with bit t = tile t after the loop.  Timing experiment: the same
-// instruction count with cheaper op types measured 0.5 % slower -- the loop is
-// bound by VALU instructions per tile, not their type
-// (profiles/r04_mf2_prio_pk_ab.txt).
-#ifndef SFM_MF2_PB
-#define SFM_MF2_PB 0
-#endif
-#ifndef SFM_MF2_PTR
-#define SFM_MF2_PTR 0
-#endif
-__device__ __forceinline__ void mf2_signs_pb(const MfZ& r, uint32_t (&sv)[16], uint32_t m) {
-#pragma unroll
-  for (int g = 0; g < 16; ++g) {
-    const uint32_t x = __builtin_amdgcn_perm(__float_as_uint(r.z2[g]), __float_as_uint(r.z1[g]), 0x0B0B0909u);
-    sv[g] = __builtin_amdgcn_bitop3_b32(sv[g], x, m, 0xF8);      // sv | (x & m)
-  }
-}
-// queue entry (candidate row << 24 | span-relative point) of string bit j:
-// bit j = tile kMf2Tiles - 1 - j (alignbit strings) or tile j (SFM_MF2_PB)
+// queue entry (candidate row << 24 | span-relative point) of the lowest set
+// bit j of a string: bit j = tile kMf2Tiles - 1 - j
 __device__ __forceinline__ uint32_t mf2_qbase(int g, int hl, int rl) {
-  return ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)((SFM_MF2_PB ? 0 : 32 * (kMf2Tiles - 1)) + rl);
+  return ((uint32_t)mf_row(g, hl) << 24) | (uint32_t)(32 * (kMf2Tiles - 1) + rl);
 }
 __device__ __forceinline__ uint32_t mf2_qentry(uint32_t base, uint32_t uu) {
-  return SFM_MF2_PB ? base + 32u * (uint32_t)__builtin_ctz(uu) : base - 32u * (uint32_t)__builtin_ctz(uu);
+  return base - 32u * (uint32_t)__builtin_ctz(uu);
 }
 // undecided evaluations of a decision-string pair
 __device__ __forceinline__ uint32_t mf2_undecided(uint32_t s1, uint32_t s2) {
@@ -630,55 +592,6 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           MfZ zA, zB;
           aB = mf2_a(mf2_load_ab(fr + (size_t)1 * kTileHalves, mf2_lane()), A1, A2);
           zA = mf2_z(mf2_load_d(fr, mf2_lane()), NL, NH, aA);
-#if SFM_MF2_PB
-          static_assert(kMf2Tiles == 32, "two 16-tile halves");
-          // s1 / s2 hold tiles 0..15 / 16..31 (both signs each) until the end
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            uint32_t (&sv)[16] = h2 ? s2 : s1;
-#pragma unroll 1
-            for (int t = 16 * h2 + 1; t < 16 * h2 + 16 && t < kMf2Tiles - 1; t += 2) {
-              const uint32_t m = 0x00010001u << ((t - 1) & 15);
-              aA = mf2_a(mf2_load_ab(fr + (size_t)(t + 1) * kTileHalves, mf2_lane()), A1, A2);
-              zB = mf2_z(mf2_load_d(fr + (size_t)t * kTileHalves, mf2_lane()), NL, NH, aB);
-              mf2_signs_pb(zA, sv, m);                                   // tile t - 1
-              aB = mf2_a(mf2_load_ab(fr + (size_t)(t + 2) * kTileHalves, mf2_lane()), A1, A2);
-              zA = mf2_z(mf2_load_d(fr + (size_t)(t + 1) * kTileHalves, mf2_lane()), NL, NH, aA);
-              mf2_signs_pb(zB, sv, m << 1);                              // tile t
-            }
-          }
-          zB = mf2_z(mf2_load_d(fr + (size_t)(kMf2Tiles - 1) * kTileHalves, mf2_lane()), NL, NH, aB);
-          mf2_signs_pb(zA, s2, 0x00010001u << 14);                       // tile 30
-          mf2_signs_pb(zB, s2, 0x00010001u << 15);                       // tile 31
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {                                 // bit t = tile t
-            const uint32_t lo = s1[g], hi = s2[g];
-            s1[g] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);          // z1 signs: lo.low16 | hi.low16 << 16
-            s2[g] = __builtin_amdgcn_perm(hi, lo, 0x07060302u);          // z2 signs: lo.high16 | hi.high16 << 16
-          }
-          if (false)
-#endif
-#if SFM_MF2_PTR
-          // one lane pointer walking the span: the four fragment loads of
-          // two tiles are immediate offsets from it, one VALU add per two
-          // tiles instead of a lane-id copy + shift-add per load.  Timing
-          // experiment: 97 instead of 104 VALU per two tiles in the loop, but
-          // the pointer costs 18 dwords of spills outside it; measured equal
-          // to 1.3 % slower (profiles/r04_mf2_prio_pk_ab.txt)
-          {
-            const _Float16* pt = fr + mf2_lane() * 8 + kTileHalves;      // tile 1, this lane
-#pragma unroll 1
-            for (int t = 1; t < kMf2Tiles - 1; t += 2, pt += 2 * kTileHalves) {
-              aA = mf2_a(mf2_load_ab(pt + kTileHalves, 0), A1, A2);        // a(t + 1)
-              zB = mf2_z(mf2_load_d(pt, 0), NL, NH, aB);                   // z(t)
-              mf2_signs(zA, s1, s2);                                       // t - 1
-              aB = mf2_a(mf2_load_ab(pt + 2 * kTileHalves, 0), A1, A2);    // a(t + 2)
-              zA = mf2_z(mf2_load_d(pt + kTileHalves, 0), NL, NH, aA);     // z(t + 1)
-              mf2_signs(zB, s1, s2);                                       // t
-            }
-          }
-          if (false)
-#endif
 #pragma unroll 1
           for (int t = 1; t < kMf2Tiles - 1; t += 2) {
 #if SFM_MF2_LN1
@@ -689,23 +602,17 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #else
 #define MF2_LN mf2_lane()
 #endif
-            MF2_PRIO_HI();
             aA = mf2_a(mf2_load_ab(fr + (size_t)(t + 1) * kTileHalves, MF2_LN), A1, A2);
             zB = mf2_z(mf2_load_d(fr + (size_t)t * kTileHalves, MF2_LN), NL, NH, aB);
-            MF2_PRIO_LO();
             mf2_signs(zA, s1, s2);
-            MF2_PRIO_HI();
             aB = mf2_a(mf2_load_ab(fr + (size_t)(t + 2) * kTileHalves, MF2_LN), A1, A2);
             zA = mf2_z(mf2_load_d(fr + (size_t)(t + 1) * kTileHalves, MF2_LN), NL, NH, aA);
-            MF2_PRIO_LO();
             mf2_signs(zB, s1, s2);
 #undef MF2_LN
           }
-#if !SFM_MF2_PB
           zB = mf2_z(mf2_load_d(fr + (size_t)(kMf2Tiles - 1) * kTileHalves, mf2_lane()), NL, NH, aB);
           mf2_signs(zA, s1, s2);
           mf2_signs(zB, s1, s2);
-#endif
         } else {
         // two accumulator sets: tile t+1's MFMAs beside tile t's decisions
         // (the last pair peeled, so the loop body has no conditional MFMA)
