@@ -159,6 +159,36 @@ def pmc_traffic(args):
     return {}, None
 
 
+def pmc_kernel_counters(traffic_src, region):
+    """The raw counters of one region of the PMC summary ``pmc_traffic``
+    matched (same workload, same sources), or None."""
+    if not traffic_src:
+        return None
+    try:
+        return json.load(open(os.path.join(ROOT, traffic_src)))["kernels"].get(region)
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+VALU_ISSUE_CYCLES = 4       # MI355X_MICROARCH.md: vector-instruction issue cost per instruction (one wave's stream)
+N_SIMD, N_XCD = 1024, 8     # 256 CUs x 4 SIMDs in 8 XCDs
+
+
+def valu_issue(counters):
+    """What bounds k_score_mf2: VALU instructions x the
+    guide's issue cost against the SIMDs' cycles over the launch, from the
+    PMC summary's SQ_INSTS_VALU and GRBM_GUI_ACTIVE (GPU-busy cycles summed
+    over the 8 XCDs; per launch).  1.0 = every SIMD issuing a VALU
+    instruction every VALU_ISSUE_CYCLES for the whole launch."""
+    if not counters or not counters.get("SQ_INSTS_VALU") or not counters.get("GRBM_GUI_ACTIVE"):
+        return None
+    cycles = counters["GRBM_GUI_ACTIVE"] / N_XCD
+    insts = counters["SQ_INSTS_VALU"]
+    return {"insts_per_launch": int(insts), "issue_cycles_per_inst": VALU_ISSUE_CYCLES,
+            "simd_cycles_per_launch": int(cycles), "frac": round(insts * VALU_ISSUE_CYCLES / (N_SIMD * cycles), 4),
+            "note": "VALU issue utilisation from the PMC summary (profiled run; SQ_INSTS_VALU includes the MFMAs)"}
+
+
 def _stats_version(path):
     """profiles/r03_kernel_stats_v4.csv -> (3, 4); a config tag (r03_kernel_stats_c3_v1.csv) is allowed."""
     m = re.search(r"r(\d+)_kernel_stats(?:_(?!v\d)([a-z0-9]+))?(?:_v(\d+))?\.csv$", os.path.basename(path))
@@ -248,7 +278,7 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
                 "mfma_issued": {"flop_per_eval": MF_MFMA_FLOP_PER_EVAL, "tflops": round(issued, 1),
                                 "frac": round(issued / PEAK_F16_TFLOPS, 4)},
                 "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work,
-                "rocprof": rp}
+                "rocprof": rp, "valu_issue": valu_issue(pmc_kernel_counters(traffic_src, "ransac_score"))}
     return {"kernel": "ransac_score (k_score32)", "bound": "valu-fp32", "achieved": round(tflops, 3),
             "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work}

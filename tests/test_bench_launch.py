@@ -155,3 +155,20 @@ def test_rocprof_kernel_match_is_whole_name(tmp_path, monkeypatch):
     assert bench.rocprof_kernel_ms(A, ("k_score_mf", "k_mf_cands"))[0] is None
     monkeypatch.setattr(bench, "src_hash", lambda: "new")
     assert bench.rocprof_kernel_ms(A, ("k_score_mf2", "k_mf_cands")) == (None, None)
+
+
+def test_valu_issue_from_pmc(tmp_path, monkeypatch):
+    """The scorer's VALU-issue utilisation comes from the same matching PMC
+    summary as `traffic`: SQ_INSTS_VALU x 4 cycles over the SIMDs' cycles
+    (GRBM_GUI_ACTIVE summed over 8 XCDs); absent counters give None."""
+    sys.path.insert(0, ROOT)
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r09_pmc_v1.json").write_text(json.dumps(
+        {"kernels": {"ransac_score": {"SQ_INSTS_VALU": 1024 * 1000, "GRBM_GUI_ACTIVE": 8 * 5000}}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    v = bench.valu_issue(bench.pmc_kernel_counters(os.path.join("profiles", "r09_pmc_v1.json"), "ransac_score"))
+    assert v["frac"] == 0.8 and v["simd_cycles_per_launch"] == 5000
+    assert bench.valu_issue(bench.pmc_kernel_counters(None, "ransac_score")) is None
+    assert bench.valu_issue({"SQ_INSTS_VALU": 5}) is None
