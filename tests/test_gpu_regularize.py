@@ -495,6 +495,11 @@ def test_channels_last_f16_exact(cuda, shape):
     got = to_channels_last(x.to(cuda), torch.float16).cpu()
     want = x.permute(0, 2, 3, 4, 1).to(torch.float16)
     assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+    # a bf16 volume (the C3 sweep's) -> f16: every bf16 value in f16 range converts exactly
+    xb = x.to(torch.bfloat16)
+    got2 = to_channels_last(xb.to(cuda), torch.float16).cpu()
+    want2 = xb.float().permute(0, 2, 3, 4, 1).to(torch.float16)
+    assert torch.equal(got2.view(torch.int16), want2.view(torch.int16))
 
 
 @pytest.mark.parametrize("B,cin,D,h,w,relu,resid,cout", [
