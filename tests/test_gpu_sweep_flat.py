@@ -167,6 +167,7 @@ def test_shared_taps_equal_gathered(cuda, dtype, B, C, L, hw, tscale, by_depth):
     (2, 16, 8, (40, 300), 0.6, False),  # windows across row and plane ends
     (1, 8, 5, (13, 64), 1.0, False),    # hw < 256: windows span several planes
     (1, 8, 5, (13, 61), 1.0, False),    # odd slab: wide stores fall back to the plain path
+    (2, 12, 6, (20, 96), 0.8, False),   # a partial channel group (C = 12, groups of 8)
 ])
 def test_wide_stores_equal_plain(cuda, dtype, B, C, L, hw, tscale, by_depth):
     """sweep_store_px (16-byte lane stores of 8 bf16 / 4 fp32 consecutive
