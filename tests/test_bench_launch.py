@@ -172,3 +172,22 @@ def test_valu_issue_from_pmc(tmp_path, monkeypatch):
     assert v["frac"] == 0.8 and v["simd_cycles_per_launch"] == 5000
     assert bench.valu_issue(bench.pmc_kernel_counters(None, "ransac_score")) is None
     assert bench.valu_issue({"SQ_INSTS_VALU": 5}) is None
+
+
+def test_rank_device_index_and_shared_gpu(monkeypatch):
+    """Each rank drives the device of its LOCAL_RANK; the shared-GPU rehearsal
+    (SFM_BENCH_SHARED_GPU=1) puts every rank on device 0."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("SFM_BENCH_SHARED_GPU", raising=False)
+    assert [bench.rank_device_index(r) for r in range(8)] == list(range(8))
+    monkeypatch.setenv("SFM_BENCH_SHARED_GPU", "1")
+    assert [bench.rank_device_index(r) for r in range(4)] == [0, 0, 0, 0]
+
+
+def test_tune_option_parses():
+    sys.path.insert(0, ROOT)
+    import bench
+    a = bench.parse(["--tune", "sweep_store_px=2,sweep_nj=2", "--config", "c3"])
+    assert a.tune == "sweep_store_px=2,sweep_nj=2" and a.config == "c3"
+    assert bench.parse([]).tune == ""
