@@ -198,14 +198,16 @@ def _stats_version(path):
     return tag, (int(m.group(1)), int(m.group(3) or 0))
 
 
-def rocprof_kernel_ms(args, prefixes):
-    """Average launch duration (ms) of the kernels named by ``prefixes`` (summed:
-    one launch each per step) from the newest committed rocprofv3 --stats
-    summary of this workload (profiles/rNN_kernel_stats[_cfg]_vK.csv, written
-    by scripts/gpu_evidence.sh from a profiled run of this bench), so the line
+def rocprof_kernel_ms(args, prefixes, optional=()):
+    """Time per step (ms) of the kernels named by ``prefixes`` (+ ``optional``
+    ones when present) from the newest committed rocprofv3 --stats summary of
+    this workload (profiles/rNN_kernel_stats[_cfg]_vK.csv, written by
+    scripts/gpu_evidence.sh from a profiled run of this bench): their total
+    durations summed over the calls of the first prefix (one launch per step;
+    the pruned scorer launches k_score_mf2 twice per step), so the line
     carries a frac that follows from the committed profile, beside the live
-    HIP-event one.  Only a summary recorded from these sources counts
-    (its .meta.json sidecar's src_hash)."""
+    HIP-event one.  Only a summary recorded from these sources counts (its
+    .meta.json sidecar's src_hash)."""
     import csv
     import glob
     best = None
@@ -216,17 +218,20 @@ def rocprof_kernel_ms(args, prefixes):
             best = (v[1], f)
     if best is None:
         return None, None
-    tot, hit = 0.0, set()
+    tot, hit, calls = 0.0, set(), {}
     with open(best[1]) as fh:
         for row in csv.DictReader(fh):
-            for p in prefixes:
+            for p in tuple(prefixes) + tuple(optional):
                 # whole kernel names: mangled (length-prefixed, "11k_score_mf2") or demangled
                 if f"{len(p)}{p}" in row["Name"] or re.search(r"\b" + re.escape(p) + r"[<(]", row["Name"]):
-                    tot += float(row["AverageNs"]) * 1e-6
+                    tot += float(row["TotalDurationNs"]) * 1e-6
+                    calls[p] = calls.get(p, 0) + int(row["Calls"])
                     hit.add(p)
                     break
     # every named kernel must be in the summary (an older scorer's profile does not count)
-    return (tot if hit == set(prefixes) else None), os.path.relpath(best[1], ROOT)
+    if not set(prefixes) <= hit or not calls.get(prefixes[0]):
+        return None, os.path.relpath(best[1], ROOT)
+    return tot / calls[prefixes[0]], os.path.relpath(best[1], ROOT)
 
 
 ROOFLINE_REGIONS = ("ransac_score", "plane_sweep", "ref_planes")
@@ -255,7 +260,8 @@ def profiled_pass(stepf, inputs, steps, dev):
     return kt
 
 
-def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, traffic_src, rocprof=None):
+def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, traffic_src, rocprof=None,
+                   scorer=None):
     """Roofline line of the RANSAC scoring kernel.  achieved = the algorithmic
     rate (SURVEY §8d: 50 FLOP per (candidate E, correspondence) evaluation);
     peak = the unit that executes it: the dense f16 MFMA peak for k_score_mf
@@ -263,17 +269,20 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
     fp32 VALU peak for k_score32.  For k_score_mf `mfma_issued` is the MFMA
     pipe's own utilisation (4 MFMAs per 1024 evaluations): the kernel's floor."""
     work = (f"{done} evals x {FLOP_PER_EVAL} FLOP per launch: {cands} candidate E x N={n} = {evals}, "
-            f"minus {skipped} skipped by exact bound pruning ({100.0 * skipped / max(evals, 1):.1f}%)")
+            f"minus {skipped} skipped by exact count-bound pruning ({100.0 * skipped / max(evals, 1):.1f}%)")
     if use_mf:
-        issued = evals * MF_MFMA_FLOP_PER_EVAL / (ms * 1e-3) / 1e12
+        issued = done * MF_MFMA_FLOP_PER_EVAL / (ms * 1e-3) / 1e12
         rp = None
         if rocprof and rocprof[0]:
             t = done * FLOP_PER_EVAL / (rocprof[0] * 1e-3) / 1e12
             rp = {"avg_launch_ms": round(rocprof[0], 4), "achieved": round(t, 3),
                   "frac": round(t / PEAK_F16_TFLOPS, 4), "source": rocprof[1],
-                  "note": "k_mf_cands + k_score_mf2 averages of the committed rocprofv3 --stats summary of this "
-                          "workload (a profiled run clocks lower than this one)"}
-        return {"kernel": "ransac_score (k_mf_cands + k_score_mf2)", "bound": "mfma-f16", "achieved": round(tflops, 3),
+                  "note": "k_mf_cands + k_score_mf2 (+ k_mf2_prune) per step from the committed rocprofv3 --stats "
+                          "summary of this workload (a profiled run clocks lower than this one)"}
+        pruned = scorer == "k_score_mf2+prune"
+        kern = ("ransac_score (k_mf_cands + k_score_mf2 x2 + k_mf2_prune: count-bound pruning)" if pruned
+                else "ransac_score (k_mf_cands + k_score_mf2)")
+        return {"kernel": kern, "scorer": scorer, "bound": "mfma-f16", "achieved": round(tflops, 3),
                 "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_F16_TFLOPS, 4),
                 "mfma_issued": {"flop_per_eval": MF_MFMA_FLOP_PER_EVAL, "tflops": round(issued, 1),
                                 "frac": round(issued / PEAK_F16_TFLOPS, 4)},
@@ -532,8 +541,7 @@ def _main_gpu(args, dist):
     done = evals - skipped                          # evaluations the launch performed
     score_ms = kt["ransac_score"]
     score_tflops = done * FLOP_PER_EVAL / (score_ms * 1e-3) / 1e12
-    use_mf = bool(_lib.tune_get("score_mf")) and not _lib.tune_get("score_mfma") and \
-        2.0 ** -15 <= args.threshold < 1.0
+    use_mf = bool(_lib.tune_get("score_mf")) and 2.0 ** -15 <= args.threshold < 1.0
     h, w = fhw
     s = 4 if cost_dtype == torch.float32 else 2
     if args.overlap_ref != "0":
@@ -580,7 +588,8 @@ def _main_gpu(args, dist):
                      "devices": names},
             "roofline": score_roofline(use_mf, score_tflops, done, evals, skipped, sum(cands), hp.n, score_ms,
                                        traffic.get("ransac_score"), traffic_src,
-                                       rocprof_kernel_ms(args, ("k_score_mf2", "k_mf_cands"))),
+                                       rocprof_kernel_ms(args, ("k_mf_cands", "k_score_mf2"),
+                                                         optional=("k_mf2_prune",)), _lib.last_scorer()),
             "roofline_sweep": {"kernel": "plane_sweep", "bound": "hbm", "achieved": round(sweep_gbs, 1),
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(sweep_gbs / PEAK_HBM_GBS, 4),
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,

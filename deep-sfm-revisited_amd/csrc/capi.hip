@@ -1,5 +1,6 @@
 // Error reporting and per-kernel event profiling for libsfm_hip.
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -16,6 +17,10 @@ Tuning& tuning() {
   static Tuning t;
   return t;
 }
+
+static std::atomic<const char*> g_last_scorer{""};
+void set_last_scorer(const char* name) { g_last_scorer.store(name, std::memory_order_relaxed); }
+const char* last_scorer() { return g_last_scorer.load(std::memory_order_relaxed); }
 
 namespace {
 struct Slot {
@@ -116,8 +121,8 @@ const TuneKey kTuneKeys[] = {
     {"score_blocks_per_cu", &sfm::Tuning::score_blocks_per_cu, v_1_64},
     {"score_fp32", &sfm::Tuning::score_fp32, v_01},
     {"score_prune", &sfm::Tuning::score_prune, v_01},
-    {"score_mfma", &sfm::Tuning::score_mfma, v_01},
     {"score_mf", &sfm::Tuning::score_mf, [](int v) { return v >= 0 && v <= 2; }},
+    {"score_mf_prune", &sfm::Tuning::score_mf_prune, [](int v) { return v == 0 || (v >= 500 && v <= 990); }},
     {"score_mf_blocks_per_cu", &sfm::Tuning::score_mf_blocks_per_cu, [](int v) { return v >= 1 && v <= 8; }},
     {"score_interleave", &sfm::Tuning::score_interleave, v_01},
     {"conv_rolling", &sfm::Tuning::conv_rolling, v_01},
@@ -149,6 +154,13 @@ int sfm_tune_get(const char* key, int* value) {
   *value = sfm::tuning().*(k->field);
   return SFM_OK;
 }
+
+const char* sfm_tune_key(int index) {
+  const int n = (int)(sizeof(kTuneKeys) / sizeof(kTuneKeys[0]));
+  return (index >= 0 && index < n) ? kTuneKeys[index].name : nullptr;
+}
+
+const char* sfm_last_scorer(void) { return sfm::last_scorer(); }
 
 int sfm_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(sfm::g_mu);

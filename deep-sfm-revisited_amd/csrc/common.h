@@ -29,9 +29,10 @@ struct Tuning {
   int score_blocks_per_cu = 32;  // persistent score grid
   int score_fp32 = 1;            // packed float32 pre-decision in the score kernel
   int score_prune = 1;           // exact bound pruning in k_score32 (PruneState)
-  int score_mfma = 0;            // 1: k_score_mx, linear forms on the matrix cores (measured 2.3x slower)
   int score_mf = 2;              // split-f16 MFMA scoring (exact by bound): 2 = k_score_mf2 (span-major, default
                                  // when num_test == num_ransac_test), 1 = k_score_mf (item-major), 0 = off
+  int score_mf_prune = 900;      // k_score_mf2 count-bound pruning: the first launch's share of each pair's
+                                 // spans in per mille (0: off; one launch)
   int score_mf_blocks_per_cu = 1; // k_score_mf persistent grid (LDS: one block per CU)
   int score_interleave = 0;      // k_score32 items: pairs interleaved (1) or pair after pair (0)
   int score_precision = 64;      // 64: exact (reference float64 decisions); 32 / 16: ComputeError<float> /
@@ -41,6 +42,11 @@ struct Tuning {
   int conv_rolling = 1;          // 1: cin-32 conv layers roll along the planes (k_conv3r); 0: k_conv3
 };
 Tuning& tuning();
+
+// The score kernel the last RANSAC / score call dispatched (sfm_last_scorer):
+// a static string literal.
+void set_last_scorer(const char* name);
+const char* last_scorer();
 
 // Profiling hooks (capi.hip): record HIP events around a launch when enabled.
 struct ProfScope {

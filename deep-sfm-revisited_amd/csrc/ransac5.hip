@@ -71,6 +71,8 @@ struct Workspace {
   int32_t* best_lb;             // [64] largest partial count seen (a lower bound on the winning score)
   unsigned long long* skipped;  // [1] evaluations skipped by pruning (whole call)
   unsigned long long* claim;    // [9] k_score_mf2's range-claim counters and finished-block count (zero between launches)
+  int32_t* cmap;       // [B][Cmax] k_mf2_prune: the kept candidates of each pair, in order
+  int32_t* cand_live;  // [64] k_mf2_prune: kept candidates per pair
   double* pack;        // [n_max][4] (last: its size is the only n_max-dependent one)
 };
 
@@ -102,6 +104,8 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   // before pack: run_packed re-lays the workspace out with n_max = 0, so every
   // field it uses must sit at an offset independent of n_max
   t.claim = (unsigned long long*)take(kMf2ClaimBytes);
+  t.cmap = (int32_t*)take(bc * C * 4);
+  t.cand_live = (int32_t*)take(SFM_MAX_BATCH * 4);
   t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
   if (w) *w = t;
   return off;
@@ -1340,269 +1344,6 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
 }
 
 // ---------------------------------------------------------------------------
-// Phase 3c: scoring on the matrix cores (k_score_mx, tuning key score_mfma).
-//
-// The float32 pre-decision of k_score32 spends 10 of its 21 VALU per
-// evaluation on five linear forms of the point:
-//   Ex0 = E0 x + E1 y + E2,  Ex1 = E3 x + E4 y + E5,  Ex2 = E6 x + E7 y + E8,
-//   xE0 = E0 x' + E3 y' + E6, xE1 = E1 x' + E4 y' + E7.
-// For a tile of 32 candidates x 32 points each is one v_mfma_f32_32x32x2_f32:
-// A = the two coefficients of the 32 candidates (K = 2), B = (x, y) or
-// (x', y') of the 32 points, and the constant term as the accumulator input
-// C (kept in registers for the whole item).  gfx950's f32 MFMA is an exact
-// fmaf chain (MI355X_MICROARCH.md), so each form has the error of a two-FMA
-// chain and k_score32's bounds (fp32_constants) hold unchanged.  The matrix
-// pipe runs beside the VALU, which keeps the remaining 12 operations per
-// evaluation (a = x'Ex0 + y'Ex1 + Ex2, D, a^2, the two decision FMAs and
-// compares, the count), so the two waves of a SIMD overlap MFMA and VALU.
-//
-// Output layout of the 32x32 MFMA: lane l, register r holds row (candidate)
-// 8 (r >> 2) + 4 (l >> 5) + (r & 3), column (point) l & 31.  Each lane keeps
-// one point and counts inliers of its 16 rows in registers; the counts are
-// reduced across the 32 lanes of each half once per item.
-//   * rows past the tile, or pruned (PruneState): A = 0, C = (0, 0, 1, 0, 0),
-//     so a = 1, D = 0: a certain outlier, never queued;
-//   * candidates outside the float32 range (ok32 = 0): A = C = 0, so a = D = 0
-//     and both compares fail: every evaluation goes to the float64 queue;
-//   * points with a coordinate beyond 2^12 (or NaN) become NaN: undecided.
-// eps per point uses the tile's largest A1, B1, A2, B2 (fp32_constants with
-// the point's M), which only widens the undecided band.
-// Only used with num_test == num_ransac_test (one count per candidate).
-//
-// Measured (scripts/prune_ab.py, scripts/pmc_kernel.sh, KITTI B=8 H=4096):
-// bit-exact, but 36.5 ms against 17.2 for k_score32, so it is off by
-// default (tuning key score_mfma).  The VALU count barely drops (23.6 against
-// 23.5 wave-instructions per 64 evaluations): the per-lane count (+2) and the
-// per-register queueing of undecided lanes take back most of the 10 FMAs the
-// matrix core removes.  And the constant accumulators plus the five outputs
-// hold 256 VGPRs, so only 2 waves share a SIMD; each wave's VALU waits on its
-// own MFMAs, and VALU issue falls to 0.29 of the cycles (0.65 for k_score32).
-// ---------------------------------------------------------------------------
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int kQueueMX = 2048;          // undecided entries per wave (a block queues at most 1024)
-
-__device__ __forceinline__ int mx_row(int r, int half) { return 8 * (r >> 2) + 4 * half + (r & 3); }
-
-template <class Src>
-__global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void k_score_mx(const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
-                const double* __restrict__ candE, int32_t* __restrict__ cntT, int32_t* __restrict__ cntR,
-                ScoreConsts kc) {
-  constexpr int kWaves = kScoreThreads / 64;
-  __shared__ int32_t s_cnt[kWaves][kKC][2];
-  __shared__ int32_t s_items[SFM_MAX_BATCH + 1];
-  __shared__ int32_t s_first[SFM_MAX_BATCH + 1];
-  __shared__ int32_t s_tiles[SFM_MAX_BATCH];
-  __shared__ double2 s_cand[kWaves][kKC * kCandStride / 2];
-  __shared__ uint32_t s_queue[kWaves][kQueueMX];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int half = lane >> 5, col = lane & 31;
-  if (tid == 0) {
-    int acc = 0;
-    for (int b = 0; b < batch; ++b) {
-      const int tiles = (cand_total[b] + kKC - 1) / kKC;
-      const int splits = (pp.test[b] + kPtsPerWave - 1) / kPtsPerWave;
-      s_tiles[b] = tiles;
-      s_items[b] = tiles * splits;
-      s_first[b] = acc;
-      acc += tiles * splits;
-    }
-    s_first[batch] = acc;
-    s_items[batch] = acc;
-  }
-  for (int i = tid; i < kWaves * kKC * 2; i += kScoreThreads) (&s_cnt[0][0][0])[i] = 0;
-  __syncthreads();
-  int32_t(*cnt)[2] = s_cnt[wv];
-  uint32_t* queue = s_queue[wv];
-  const double* CE = reinterpret_cast<const double*>(s_cand[wv]);
-  const float nt2lo = -kc.t2lo32, nt2hi = -kc.t2hi32;
-  const int total = __builtin_amdgcn_readfirstlane(s_items[batch]);
-  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
-  unsigned long long skipped = 0;
-  for (int item = gw; item < total; item += gridDim.x * kWaves) {
-    int b = 0;
-    while (item >= s_first[b + 1]) ++b;
-    b = __builtin_amdgcn_readfirstlane(b);
-    const int local = item - __builtin_amdgcn_readfirstlane(s_first[b]);
-    const int tiles = __builtin_amdgcn_readfirstlane(s_tiles[b]);
-    const int split = local / tiles, tile = local - split * tiles;
-    const int ctot = cand_total[b];
-    const int c0 = tile * kKC;
-    const int nc = min(kKC, ctot - c0);
-    const int T = pp.test[b], R = pp.rtest[b];
-    const int p0 = split * kPtsPerWave;
-    const int p1 = min(T, p0 + kPtsPerWave);
-    {
-      const double2* srcc = reinterpret_cast<const double2*>(candE + ((size_t)b * cmax + c0) * kCandStride);
-      for (int i = lane; i < nc * (kCandStride / 2); i += 64) s_cand[wv][i] = srcc[i];
-    }
-    wave_sync();
-    bool all_pruned = false;
-    int lb = 0;
-    if (kc.prune) {
-      const PruneState st = prune_state(cntR, kc.ws_batch, cmax);
-      lb = __hip_atomic_load(st.best_lb + (size_t)b * kBestStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      bool pr = false;
-      if (lane < nc) {
-        const unsigned long long v = __hip_atomic_load(st.cov + (size_t)b * cmax + c0 + lane, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        pr = (long long)(uint32_t)v + (long long)T - (long long)(v >> 32) < (long long)lb;
-        if (pr) reinterpret_cast<float*>(s_cand[wv])[(lane * kCandStride + 10) * 2 + 13] = __uint_as_float(kPrunedFlag);
-      }
-      all_pruned = __ballot(pr) == lane_prefix(nc);
-      wave_sync();
-    }
-    int qn = 0;
-    if (!all_pruned) {
-      // A operands: candidate `col`, coefficient `half`; tile eps constants (max over live rows)
-      float aex0 = 0.0f, aex1 = 0.0f, aex2 = 0.0f, axe0 = 0.0f, axe1 = 0.0f;
-      float A1 = 0.0f, B1 = 0.0f, A2 = 0.0f, B2 = 0.0f;
-      if (col < nc) {
-        const float* F = reinterpret_cast<const float*>(CE + (size_t)col * kCandStride + 10);
-        const uint32_t ok = __float_as_uint(F[13]);
-        if (ok != 0u && ok != kPrunedFlag) {
-          aex0 = half ? F[1] : F[0];
-          aex1 = half ? F[4] : F[3];
-          aex2 = half ? F[7] : F[6];
-          axe0 = half ? F[3] : F[0];
-          axe1 = half ? F[4] : F[1];
-          A1 = F[9]; B1 = F[10]; A2 = F[11]; B2 = F[12];
-        }
-      }
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        A1 = fmaxf(A1, __shfl_xor(A1, d, 64));
-        B1 = fmaxf(B1, __shfl_xor(B1, d, 64));
-        A2 = fmaxf(A2, __shfl_xor(A2, d, 64));
-        B2 = fmaxf(B2, __shfl_xor(B2, d, 64));
-      }
-      // accumulator inputs: the constant terms of this lane's 16 rows
-      f32x16 cex0, cex1, cex2, cxe0, cxe1;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = mx_row(r, half);
-        float v0 = 0.0f, v1 = 0.0f, v2 = 1.0f, v3 = 0.0f, v4 = 0.0f;   // dead row: a = 1, D = 0
-        if (i < nc) {
-          const float* F = reinterpret_cast<const float*>(CE + (size_t)i * kCandStride + 10);
-          const uint32_t ok = __float_as_uint(F[13]);
-          if (ok == 0u) {
-            v2 = 0.0f;                                                  // float64 path for every point
-          } else if (ok != kPrunedFlag) {
-            v0 = F[2]; v1 = F[5]; v2 = F[8]; v3 = F[6]; v4 = F[7];
-          }
-        }
-        cex0[r] = v0; cex1[r] = v1; cex2[r] = v2; cxe0[r] = v3; cxe1[r] = v4;
-      }
-      uint32_t cntv[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) cntv[r] = 0u;
-      // points of the next two blocks are loaded ahead (a block is only 16
-      // evaluations per lane, far shorter than an L2 round trip)
-      double4 v_next[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) v_next[k] = src.load(b, min(p0 + 32 * k + col, p1 - 1));
-      for (int cb = p0; cb < p1; cb += 32) {
-        if (qn > kQueueMX - 1024) {                      // drain before a block could overflow the queue
-          wave_sync();
-          score32_drain(CE, src, b, p0, T, R, kc, lane, cnt, queue, qn);
-          qn = 0;
-          wave_sync();
-        }
-        const int p = cb + col;
-        const bool live = p < p1;
-        const double4 v = v_next[0];
-        v_next[0] = v_next[1];
-        v_next[1] = src.load(b, min(p + 64, p1 - 1));
-        float x = (float)v.x, y = (float)v.y, xp = (float)v.z, yp = (float)v.w;
-        // M = max(1, |coordinates|) from the float32 copies: for M = 1 exactly the
-        // float64 bound; otherwise within 2^-24 relative, inside the 2^-20 slack of A*, B*
-        const float Mx = fmaxf(1.0f, fmaxf(fmaxf(fabsf(x), fabsf(y)), fmaxf(fabsf(xp), fabsf(yp))));
-        const bool bad = !(Mx <= 0x1p12f);
-        const float qnan = __builtin_nanf("");
-        if (bad) { x = qnan; y = qnan; xp = qnan; yp = qnan; }
-        const float Mf = bad ? 1.0f : Mx;
-        const float M2 = Mf * Mf, M4 = M2 * M2;
-        const float neps1 = -__builtin_fmaf(A1, M4, B1 * M2);
-        const float eps2 = __builtin_fmaf(A2, M4, B2 * M2);
-        const float bx = half ? y : x, bxp = half ? yp : xp;
-        const f32x16 ex0 = __builtin_amdgcn_mfma_f32_32x32x2f32(aex0, bx, cex0, 0, 0, 0);
-        const f32x16 ex1 = __builtin_amdgcn_mfma_f32_32x32x2f32(aex1, bx, cex1, 0, 0, 0);
-        const f32x16 ex2 = __builtin_amdgcn_mfma_f32_32x32x2f32(aex2, bx, cex2, 0, 0, 0);
-        const f32x16 xe0 = __builtin_amdgcn_mfma_f32_32x32x2f32(axe0, bxp, cxe0, 0, 0, 0);
-        const f32x16 xe1 = __builtin_amdgcn_mfma_f32_32x32x2f32(axe1, bxp, cxe1, 0, 0, 0);
-        const uint64_t lmask = __ballot(live);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float a = __builtin_fmaf(xp, ex0[r], __builtin_fmaf(yp, ex1[r], ex2[r]));
-          const float D = __builtin_fmaf(xe1[r], xe1[r], __builtin_fmaf(xe0[r], xe0[r],
-                                         __builtin_fmaf(ex1[r], ex1[r], ex0[r] * ex0[r])));
-          const float aa = a * a;
-          const float din = __builtin_fmaf(nt2lo, D, aa);
-          const float dout = __builtin_fmaf(nt2hi, D, aa);
-          const bool in = din < neps1 && live;
-          cntv[r] += in ? 1u : 0u;
-          const uint64_t und = ~(__ballot(din < neps1) | __ballot(dout > eps2)) & lmask;
-          if (und) {                                      // wave-uniform
-            if ((und >> lane) & 1ull) {
-              const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(und >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)und, 0));
-              queue[pos] = ((uint32_t)mx_row(r, half) << 24) | (uint32_t)(p - p0);   // relative to the item
-            }
-            qn += __popcll(und);
-          }
-        }
-      }
-      wave_sync();
-      score32_drain(CE, src, b, p0, T, R, kc, lane, cnt, queue, qn);
-      wave_sync();
-      // per-row totals: sum over the 32 lanes of each half
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        uint32_t s = cntv[r];
-#pragma unroll
-        for (int d = 16; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-        if (col == 0) {
-          const int i = mx_row(r, half);
-          cnt[i][0] += (int)s;
-          cnt[i][1] += (int)s;
-        }
-      }
-      wave_sync();
-    }
-    if (kc.prune) {
-      const PruneState st = prune_state(cntR, kc.ws_batch, cmax);
-      int reached = 0, skip = 0;
-      if (lane < nc) {
-        const float* F = reinterpret_cast<const float*>(CE + (size_t)lane * kCandStride + 10);
-        if (__float_as_uint(F[13]) == kPrunedFlag) {
-          skip = p1 - p0;
-        } else {
-          const int sc = cnt[lane][0];
-          const unsigned long long old = atomicAdd(st.cov + (size_t)b * cmax + c0 + lane,
-                                                   ((unsigned long long)(p1 - p0) << 32) | (unsigned)sc);
-          reached = (int)(uint32_t)old + sc;
-        }
-      }
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        reached = max(reached, __shfl_xor(reached, d, 64));
-        skip += __shfl_xor(skip, d, 64);
-      }
-      if (lane == 0 && reached > lb) atomicMax(st.best_lb + (size_t)b * kBestStride, reached);
-      skipped += (unsigned long long)skip;
-    }
-    {
-      const int c = lane >> 1, which = lane & 1;
-      const int s = cnt[c][which];
-      cnt[c][which] = 0;                                  // every row: dead rows may hold counts
-      if (c < nc && s) atomicAdd((which ? cntR : cntT) + (size_t)b * cmax + c0 + c, s);
-    }
-    wave_sync();
-  }
-  if (kc.prune && lane == 0 && skipped) atomicAdd(prune_state(cntR, kc.ws_batch, cmax).skipped, skipped);
-}
-
-// ---------------------------------------------------------------------------
 // Phase 4: selection (one block per pair)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_select(int H, int cmax, int cheir,
@@ -1794,6 +1535,9 @@ struct ScoreBufs {
   int32_t* cntT;
   int32_t* cntR;
   unsigned long long* claim;   // [9] k_score_mf2's range-claim counters and finished-block count
+  int32_t* cmap = nullptr;     // count-bound pruning (k_mf2_prune): kept candidates, their number,
+  int32_t* cand_live = nullptr;   // the evaluations skipped
+  unsigned long long* skipped = nullptr;
 };
 
 // score_precision with the low-precision form folded in: 64, 32 / 16 (held in
@@ -1806,44 +1550,64 @@ static int lowp_prec() {
 template <class Src>
 static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cmax, const ScoreBufs& w,
                            const ScoreConsts& kc, const MfParams& mp, bool use_mf, bool same, int prec, bool fast,
-                           bool fast32, int cus, int grid, hipStream_t s) {
+                           bool fast32, int cus, int grid, hipStream_t s, int prune_pm = 0) {
   if (use_mf) {
     hipLaunchKernelGGL(k_mf_cands, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax, w.cand_total, w.candE,
                        w.candF, mp, w.claim);
     const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
-    if (same && tuning().score_mf == 2)
-      hipLaunchKernelGGL(k_score_mf2<Src>, dim3(std::max(1, cus)), dim3(kMf2Waves * 64), 0, s, src, pp, bc, cmax,
-                         w.cand_total, w.candE, w.candF, w.cntT, kc, w.claim);
-    else if (same)
+    const dim3 g2(std::max(1, cus)), b2(kMf2Waves * 64);
+    if (same && tuning().score_mf == 2 && prune_pm > 0) {
+      // count-bound pruning: every candidate on the first prune_pm per mille
+      // of each pair's spans, k_mf2_prune, the kept ones on the rest
+      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
+                         kc, w.claim, (const int32_t*)nullptr, 0, prune_pm);
+      hipLaunchKernelGGL(k_mf2_prune<Src>, dim3(bc), dim3(1024), 0, s, src, pp, cmax, prune_pm, w.cand_total,
+                         w.candE, w.cntT, kc, w.cand_live, w.cmap, w.skipped);
+      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_live, w.candE, w.candF, w.cntT,
+                         kc, w.claim, (const int32_t*)w.cmap, prune_pm, 1000);
+      set_last_scorer("k_score_mf2+prune");
+    } else if (same && tuning().score_mf == 2) {
+      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
+                         kc, w.claim, (const int32_t*)nullptr, 0, 1000);
+      set_last_scorer("k_score_mf2");
+    } else if (same) {
       hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
-    else
+      set_last_scorer("k_score_mf");
+    } else {
       hipLaunchKernelGGL((k_score_mf<Src, false>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
                          w.cand_total, w.candE, w.candF, w.cntT, w.cntR, kc);
-  } else if (prec == 32)
+      set_last_scorer("k_score_mf");
+    }
+  } else if (prec == 32) {
     hipLaunchKernelGGL((k_score<false, Src, 32>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                        w.cand_total, w.candE, w.cntT, w.cntR, kc);
-  else if (prec == 16)
+    set_last_scorer("k_score<32>");
+  } else if (prec == 16) {
     hipLaunchKernelGGL((k_score<false, Src, 16>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                        w.cand_total, w.candE, w.cntT, w.cntR, kc);
-  else if (prec == 33)
+    set_last_scorer("k_score<16>");
+  } else if (prec == 33) {
     hipLaunchKernelGGL((k_score<false, Src, 33>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                        w.cand_total, w.candE, w.cntT, w.cntR, kc);
-  else if (prec == 17)
+    set_last_scorer("k_score<33>");
+  } else if (prec == 17) {
     hipLaunchKernelGGL((k_score<false, Src, 17>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                        w.cand_total, w.candE, w.cntT, w.cntR, kc);
-  else if (fast32 && same && tuning().score_mfma)
-    hipLaunchKernelGGL(k_score_mx<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax, w.cand_total,
-                       w.candE, w.cntT, w.cntR, kc);
-  else if (fast32)
+    set_last_scorer("k_score<17>");
+  } else if (fast32) {
     hipLaunchKernelGGL(k_score32<Src>, dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax, w.cand_total,
                        w.candE, w.cntT, w.cntR, kc);
-  else if (fast)
+    set_last_scorer(kc.prune ? "k_score32+prune" : "k_score32");
+  } else if (fast) {
     hipLaunchKernelGGL((k_score<true, Src>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                        w.cand_total, w.candE, w.cntT, w.cntR, kc);
-  else
+    set_last_scorer("k_score<fma>");
+  } else {
     hipLaunchKernelGGL((k_score<false, Src>), dim3(grid), dim3(kScoreThreads), 0, s, src, pp, bc, cmax,
                        w.cand_total, w.candE, w.cntT, w.cntR, kc);
+    set_last_scorer("k_score<ref>");
+  }
 }
 
 // Candidate records of given essential matrices (sfm_score_essentials): E,
@@ -2012,8 +1776,14 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   bool same = true;
   for (int b = 0; b < bc; ++b) same = same && pp.test[b] == pp.rtest[b];
   MfParams mp{};
-  const bool use_mf = fast32 && tuning().score_mf && !tuning().score_mfma && mf_params(thr, &mp);
+  const bool use_mf = fast32 && tuning().score_mf && mf_params(thr, &mp);
   kc.prune = (fast32 && !use_mf && same && !score_out && tuning().score_prune) ? 1 : 0;
+  // count-bound pruning in k_score_mf2 (k_mf2_prune): same condition, and
+  // every pair long enough that the second launch has spans to skip
+  int min_spans = INT32_MAX;
+  for (int b = 0; b < bc; ++b) min_spans = std::min(min_spans, mf2_spans(std::max(pp.test[b], pp.rtest[b])));
+  const int mf2_pm = (use_mf && same && !score_out && tuning().score_mf == 2 && min_spans >= kMf2PruneMinSpans)
+                         ? tuning().score_mf_prune : 0;
   kc.ws_batch = ws_batch;
   kc.interleave = tuning().score_interleave;
   SFM_REQUIRE(prune_state(w.cntR, ws_batch, cmax).skipped == w.skipped, "internal: pruning state layout");
@@ -2024,8 +1794,11 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   if (g_score_fence_on && g_score_fence) SFM_HIP(hipEventRecord(g_score_fence, s));
   {
     ProfScope ps("ransac_score", s);
-    score_dispatch(src, pp, bc, cmax, ScoreBufs{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim}, kc, mp, use_mf,
-                   same, prec, fast, fast32, cus, grid, s);
+    ScoreBufs sb{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim};
+    sb.cmap = w.cmap;
+    sb.cand_live = w.cand_live;
+    sb.skipped = w.skipped;
+    score_dispatch(src, pp, bc, cmax, sb, kc, mp, use_mf, same, prec, fast, fast32, cus, grid, s, mf2_pm);
   }
   SFM_LAUNCHED();
   {
@@ -2216,7 +1989,7 @@ int sfm_score_essentials(const double* pts, int64_t n_stride, const int64_t* n, 
   kc.ws_batch = batch;
   kc.interleave = tuning().score_interleave;
   MfParams mp{};
-  const bool use_mf = fast32 && tuning().score_mf && !tuning().score_mfma && mf_params(thr, &mp);
+  const bool use_mf = fast32 && tuning().score_mf && mf_params(thr, &mp);
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = std::max(1, cus) * tuning().score_blocks_per_cu;

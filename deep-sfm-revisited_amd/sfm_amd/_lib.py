@@ -107,6 +107,8 @@ _SIGS = [
       ctypes.c_size_t, _c_dp]),
     ("sfm_tune_set", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("sfm_tune_get", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+    ("sfm_tune_key", ctypes.c_char_p, [ctypes.c_int]),
+    ("sfm_last_scorer", ctypes.c_char_p, []),
     ("sfm_profile_enable", ctypes.c_int, [ctypes.c_int]),
     ("sfm_profile_select", ctypes.c_int, [ctypes.c_char_p]),
     ("sfm_profile_reset", ctypes.c_int, []),
@@ -199,3 +201,29 @@ def tune_get(key):
     v = ctypes.c_int(0)
     check(load().sfm_tune_get(key.encode(), ctypes.byref(v)), "sfm_tune_get")
     return v.value
+
+
+def tune_keys():
+    """Every tuning key of the library, in its own order (sfm_tune_key)."""
+    keys, i = [], 0
+    while True:
+        k = load().sfm_tune_key(i)
+        if k is None:
+            return keys
+        keys.append(k.decode())
+        i += 1
+
+
+def tune_snapshot():
+    """{key: value} of every tuning knob (restore with tune_restore)."""
+    return {k: tune_get(k) for k in tune_keys()}
+
+
+def tune_restore(snap):
+    for k, v in snap.items():
+        tune(k, v)
+
+
+def last_scorer():
+    """The score kernel the last RANSAC / score call dispatched (sfm_last_scorer)."""
+    return load().sfm_last_scorer().decode()

@@ -414,11 +414,18 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *     "score_mf"              0..2    split-f16 matrix-core scorers (2: span-major
  *                                     k_score_mf2, 1: k_score_mf, 0: VALU scorers;
  *                                     2 by default; exact by proof, same counts)
+ *     "score_mf_prune"        0, 500..990  count-bound pruning in k_score_mf2 (900):
+ *                                     every candidate scored on the first N per
+ *                                     mille of each pair's 1024-point spans, then
+ *                                     only candidates whose bound can still reach
+ *                                     the leader's exact count (k_mf2_prune); 0 =
+ *                                     one launch.  Winner, count, E, P unchanged;
+ *                                     only with num_test == num_ransac_test, no
+ *                                     per-hypothesis scores, >= 32 spans per pair
  *     "roots_split"           0, 1, 2 k_roots_split: falsi nodes shared by the wave's
  *                                     64 lanes (1, default), or by the four waves of
  *                                     a block (2, measured 2-6 % slower), speculated
  *                                     fallback bisection; same bits as k_roots (0)
- *     "score_mfma"            0, 1    f32 matrix-core scorer k_score_mx (0; exact, slower)
  *     "conv_rolling"          0, 1    rolling-plane Conv3d for cin 32 (1; same bits)
  *
  *   results MAY change (sweep outputs by FMA rounding only):
@@ -445,6 +452,15 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
 int sfm_tune_set(const char* key, int value);
 /* The current value of a tuning key. */
 int sfm_tune_get(const char* key, int* value);
+/* The name of tuning key `index` (0, 1, ...), NULL past the last one: lets a
+ * caller snapshot and restore every knob (tests/conftest.py does, around
+ * each GPU test). */
+const char* sfm_tune_key(int index);
+/* The score kernel the most recent RANSAC / score call of this process
+ * dispatched ("k_score_mf2", "k_score_mf", "k_score32", ...; "" before any),
+ * followed by "+prune" when k_score_mf2 ran with count-bound pruning (two
+ * launches and k_mf2_prune between them).  A dispatch check for tests. */
+const char* sfm_last_scorer(void);
 
 /* ------------------------------------------------------------------------
  * Per-kernel timing (HIP events recorded around every launch on the

@@ -18,6 +18,26 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU test")
 
 
+@pytest.fixture(autouse=True)
+def _tuning_isolated(request):
+    """Every GPU test runs on the library's tuning state as the session found
+    it and leaves it so: every knob (sfm_tune_key's list) is snapshotted before
+    the test and restored after it, so a test that switches a scorer or a
+    launch shape cannot leak that choice into the tests after it (round 4 ran
+    the C2 and band-edge parity tests on k_score_mf after one did)."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from sfm_amd import _lib
+    try:
+        snap = _lib.tune_snapshot()
+    except _lib.SfmError:
+        snap = None
+    yield
+    if snap is not None:
+        _lib.tune_restore(snap)
+
+
 @pytest.fixture(scope="session", autouse=True)
 def _build_oracle():
     # the oracle is test infrastructure: build it if the .so is missing

@@ -154,7 +154,8 @@ def test_tuning_keys_round_trip():
     doc = open(os.path.join(ROOT, "include", "sfm_hip.h")).read()
     block = doc[doc.index("Tuning knobs"):doc.index("int sfm_tune_set")]
     keys = re.findall(r'"([a-z0-9_]+)"', block)
-    assert len(set(keys)) == 25 and "score_lowp_template" in keys and "solve_coop" in keys and "score_mf" in keys and "roots_split" in keys and "sweep_buffer" in keys
+    assert set(keys) == set(_lib.tune_keys())           # documented == exported (sfm_tune_key)
+    assert len(set(keys)) == 25 and "score_mf_prune" in keys and "score_lowp_template" in keys
     for k in keys:
         _lib.tune_get(k)
     old = _lib.tune_get("sweep_nj")
@@ -168,6 +169,10 @@ def test_tuning_keys_round_trip():
         _lib.tune("sweep_nj", old)
     with pytest.raises(Exception):
         _lib.tune_get("no_such_knob")
+    snap = _lib.tune_snapshot()
+    assert snap["score_mf"] == 2 and snap["score_mf_prune"] == 900
+    _lib.tune_restore(snap)
+    assert _lib.load().sfm_tune_key(-1) is None and _lib.last_scorer() == ""
 
 
 def test_profile_select_filters_names():

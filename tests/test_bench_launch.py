@@ -150,11 +150,20 @@ def test_rocprof_kernel_match_is_whole_name(tmp_path, monkeypatch):
     class A:
         config = "c2"
     # v2 has no .meta.json (recorded from unknown sources): only v1 counts
-    ms, src = bench.rocprof_kernel_ms(A, ("k_score_mf2", "k_mf_cands"))
+    ms, src = bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf2"))
     assert abs(ms - 5.01) < 1e-9 and src.endswith("r09_kernel_stats_v1.csv")
-    assert bench.rocprof_kernel_ms(A, ("k_score_mf", "k_mf_cands"))[0] is None
+    assert bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf"))[0] is None
+    # the pruned scorer: two k_score_mf2 launches and one k_mf2_prune per step
+    (prof / "r09_kernel_stats_v3.csv").write_text(
+        '"Name","Calls","TotalDurationNs","AverageNs"\n'
+        '"_ZN3sfm11k_score_mf2INS_9PackedSrcEEEvT_",4,10000000,2500000\n'
+        '"_ZN3sfm11k_mf2_pruneINS_9PackedSrcEEEvT_",2,40000,20000\n'
+        '"_ZN3sfm10k_mf_candsEiPKi",2,20000,10000\n')
+    (prof / "r09_kernel_stats_v3.meta.json").write_text(json.dumps({"src_hash": "cur"}))
+    ms, src = bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf2"), optional=("k_mf2_prune",))
+    assert abs(ms - 5.03) < 1e-9 and src.endswith("r09_kernel_stats_v3.csv")
     monkeypatch.setattr(bench, "src_hash", lambda: "new")
-    assert bench.rocprof_kernel_ms(A, ("k_score_mf2", "k_mf_cands")) == (None, None)
+    assert bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf2")) == (None, None)
 
 
 def test_valu_issue_from_pmc(tmp_path, monkeypatch):

@@ -1,10 +1,17 @@
-"""Exact bound pruning in the float32 score kernel k_score32 (tuning key
-score_prune; the split-f16 matrix-core scorer k_score_mf, the default, is
-turned off here with score_mf=0): the
-winner, its inlier count, E and P must be identical with pruning on and off,
-and (through the unpruned path's bit-exact parity) equal to the oracle's.
-Pruning is active only without per-hypothesis scores and with
-num_test == num_ransac_test (SFMnet's call)."""
+"""Exact count-bound pruning, in both scorers that have it:
+
+  * k_score_mf2 (the default and benched scorer; tuning key score_mf_prune):
+    every candidate scored on the first 900 per mille of each pair's spans,
+    k_mf2_prune keeps the candidates whose bound can still reach the leader's
+    exact count, a second launch scores those on the rest;
+  * k_score32 (the float32 VALU scorer, score_mf=0; tuning key score_prune,
+    PruneState).
+
+The winner, its inlier count, E and P must be identical with pruning on and
+off, and (through the unpruned path's bit-exact parity) equal to the
+oracle's.  Pruning is active only without per-hypothesis scores and with
+num_test == num_ransac_test (SFMnet's call).  Every call asserts the kernel
+it dispatched."""
 import numpy as np
 import pytest
 import torch
@@ -14,22 +21,27 @@ from oracle import ransac5 as R
 pytestmark = pytest.mark.gpu
 
 
-def _both(pts, n=None, iters=2, thr=1e-4, nt=None, nr=None):
+def _both(pts, n=None, iters=2, thr=1e-4, nt=None, nr=None, scorer="mf2"):
+    """{0: unpruned, 1: pruned} -> (E, P, inliers, winner, skipped evaluations)."""
     from sfm_amd import _lib, ransac
     B = pts.shape[0]
     ws = ransac.workspace_for(B, iters, pts.device)
-    out = {}
+    out, kernels = {}, {}
+    snap = _lib.tune_snapshot()
     try:
-        _lib.tune("score_mf", 0)
+        _lib.tune("score_mf", 2 if scorer == "mf2" else 0)
         for prune in (0, 1):
-            _lib.tune("score_prune", prune)
+            if scorer == "mf2":
+                _lib.tune("score_mf_prune", 900 if prune else 0)
+            else:
+                _lib.tune("score_prune", prune)
             E, P, inl, win = ransac.ransac5_batched(pts, n, nt, nr, iters, thr, workspace=ws)
             torch.cuda.synchronize()
+            kernels[prune] = _lib.last_scorer()
             out[prune] = (E.cpu(), P.cpu(), inl.cpu(), win.cpu(), ransac.skipped_evaluations(ws, B, iters))
     finally:
-        _lib.tune("score_prune", 1)
-        _lib.tune("score_mf", 1)
-    return out
+        _lib.tune_restore(snap)
+    return out, kernels
 
 
 def _same(out):
@@ -39,23 +51,63 @@ def _same(out):
     assert a[4] == 0
 
 
-def test_pruning_full_size_kitti(cuda):
+@pytest.mark.parametrize("scorer", ["mf2", "k32"])
+def test_pruning_full_size_kitti(cuda, scorer):
     """The bench workload shape: 2 KITTI pairs, N = 435,032, H = 4096."""
     from sfm_amd import ransac, synth
     flow, K, _, _ = synth.kitti_pair_batch(2, seed=1000, device=cuda)
     pts = ransac.flow_to_points(flow, torch.inverse(K))
-    out = _both(pts, iters=8)
+    out, kernels = _both(pts, iters=8, scorer=scorer)
+    if scorer == "mf2":
+        assert kernels == {0: "k_score_mf2", 1: "k_score_mf2+prune"}
+    else:
+        assert kernels == {0: "k_score32", 1: "k_score32+prune"}
     _same(out)
     assert out[1][4] > 0                                  # pruning engaged on real data
     assert int(out[1][2].min()) > 10000
 
 
-@pytest.mark.parametrize("seed", [3, 11])
-def test_pruning_matches_oracle_winner(cuda, seed):
+def test_mf2_pruning_full_size_vs_oracle(cuda):
+    """One full KITTI pair through the default (pruned) launch against the
+    oracle, with the share of skipped evaluations reported."""
     from sfm_amd import ransac, synth
-    flow, K, _, _ = synth.kitti_pair_batch(1, seed=seed, hw=(120, 200), device=cuda)
+    flow, K, _, _ = synth.kitti_pair_batch(1, seed=1000, device=cuda)
     pts = ransac.flow_to_points(flow, torch.inverse(K))
-    out = _both(pts, iters=2)
+    out, kernels = _both(pts, iters=8)
+    assert kernels[1] == "k_score_mf2+prune"
+    _same(out)
+    p = pts[0].cpu().numpy()
+    ref = R.ransac5(p[:, :2], p[:, 2:], iters=8, thr=1e-4, nthreads=16)
+    E, P, inl, win, skipped = out[1]
+    assert int(win[0]) == ref["winner"] and int(inl[0]) == ref["inliers"]
+    assert np.array_equal(E[0].numpy(), ref["E"]) and np.array_equal(P[0].numpy(), ref["P"])
+    total = int(ref["hyp_ncand"].clip(min=1).sum()) * p.shape[0]
+    print(f"skipped {skipped} of {total} evaluations ({100.0 * skipped / total:.1f} %)")
+    assert skipped > 0.03 * total
+
+
+@pytest.mark.parametrize("pm", [500, 800, 990])
+def test_mf2_pruning_split_points(cuda, pm):
+    """Other first-launch shares (the key's range): the same results."""
+    from sfm_amd import _lib, ransac, synth
+    flow, K, _, _ = synth.kitti_pair_batch(1, seed=5, hw=(200, 400), device=cuda)
+    pts = ransac.flow_to_points(flow, torch.inverse(K))
+    ref = ransac.ransac5_batched(pts, None, None, None, 2, 1e-3, return_scores=True)
+    _lib.tune("score_mf_prune", pm)
+    got = ransac.ransac5_batched(pts, None, None, None, 2, 1e-3)
+    assert _lib.last_scorer() == "k_score_mf2+prune"
+    for x, y in zip(got, ref[:4]):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("seed", [3, 11])
+@pytest.mark.parametrize("scorer", ["mf2", "k32"])
+def test_pruning_matches_oracle_winner(cuda, seed, scorer):
+    from sfm_amd import ransac, synth
+    flow, K, _, _ = synth.kitti_pair_batch(1, seed=seed, hw=(200, 320), device=cuda)
+    pts = ransac.flow_to_points(flow, torch.inverse(K))
+    out, kernels = _both(pts, iters=2, scorer=scorer)
+    assert kernels[1].endswith("+prune")
     _same(out)
     p = pts[0].cpu().numpy()
     ref = R.ransac5(np.ascontiguousarray(p[:, :2]), np.ascontiguousarray(p[:, 2:]), iters=2, thr=1e-4, nthreads=16)
@@ -65,44 +117,36 @@ def test_pruning_matches_oracle_winner(cuda, seed):
     assert np.array_equal(P[0].numpy(), ref["P"])
 
 
-def test_pruning_ragged_batch(cuda):
-    """Pairs with different point counts (interleaved items, per-pair bounds)."""
+@pytest.mark.parametrize("scorer", ["mf2", "k32"])
+def test_pruning_ragged_batch(cuda, scorer):
+    """Pairs with different point counts (per-pair split points and bounds)."""
     from sfm_amd import ransac, synth
-    flow, K, _, _ = synth.kitti_pair_batch(3, seed=21, hw=(100, 180), device=cuda)
+    flow, K, _, _ = synth.kitti_pair_batch(3, seed=21, hw=(240, 400), device=cuda)
     pts = ransac.flow_to_points(flow, torch.inverse(K))
     N = pts.shape[1]
-    out = _both(pts, n=[N, N // 3, 2 * N // 3], iters=2)
+    out, kernels = _both(pts, n=[N, N // 2, 2 * N // 3], iters=2, scorer=scorer)
+    assert kernels[1].endswith("+prune")
     _same(out)
 
 
-def test_pruning_off_when_prefixes_differ(cuda):
+def test_mf2_pruning_off_for_short_pairs(cuda):
+    """Pairs under 32 spans (e.g. 2,048 keypoints) run one launch."""
+    from sfm_amd import _lib, ransac, synth
+    flow, K, _, _ = synth.kitti_pair_batch(1, seed=5, hw=(100, 160), device=cuda)
+    pts = ransac.flow_to_points(flow, torch.inverse(K))
+    ransac.ransac5_batched(pts, None, None, None, 2, 1e-4)
+    assert _lib.last_scorer() == "k_score_mf2"
+
+
+@pytest.mark.parametrize("scorer", ["mf2", "k32"])
+def test_pruning_off_when_prefixes_differ(cuda, scorer):
     """num_test != num_ransac_test: the preselection count differs from the
     score, so the bound does not apply and nothing is skipped."""
     from sfm_amd import ransac, synth
-    flow, K, _, _ = synth.kitti_pair_batch(1, seed=5, hw=(100, 160), device=cuda)
+    flow, K, _, _ = synth.kitti_pair_batch(1, seed=5, hw=(200, 320), device=cuda)
     pts = ransac.flow_to_points(flow, torch.inverse(K))
     N = pts.shape[1]
-    out = _both(pts, iters=2, nt=N // 2, nr=N)
+    out, kernels = _both(pts, iters=2, nt=N // 2, nr=N, scorer=scorer)
+    assert not kernels[1].endswith("+prune")
     _same(out)
     assert out[1][4] == 0
-
-
-def test_mfma_scorer_is_exact(cuda):
-    """The matrix-core scorer (tuning key score_mfma, off by default) gives the
-    same per-hypothesis scores as the VALU scorer, hence the oracle's."""
-    from sfm_amd import _lib, ransac, synth
-    flow, K, _, _ = synth.kitti_pair_batch(2, seed=8, hw=(120, 200), device=cuda)
-    pts = ransac.flow_to_points(flow, torch.inverse(K))
-    outs = []
-    try:
-        for mx in (0, 1):
-            _lib.tune("score_mfma", mx)
-            outs.append(ransac.ransac5_batched(pts, iters=2, threshold=1e-4, return_scores=True))
-            torch.cuda.synchronize()
-    finally:
-        _lib.tune("score_mfma", 0)
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a.cpu(), b.cpu())
-    p = pts[0].cpu().numpy()
-    ref = R.ransac5(np.ascontiguousarray(p[:, :2]), np.ascontiguousarray(p[:, 2:]), iters=2, thr=1e-4, nthreads=16)
-    assert np.array_equal(outs[1][4][0].cpu().numpy(), ref["hyp_score"])

@@ -137,15 +137,19 @@ def test_full_size_dense_pair(cuda):
 
 
 def test_full_size_kitti_h4096_vs_oracle(cuda):
-    """C2 at full size: one KITTI pair, N = 435,032, H = 4096 (ransac_iter 8).
-    The default launch (exact bound pruning on) and the per-hypothesis-score
-    launch (pruning off) both give the oracle's winner, count, E and P; the
-    latter also every hypothesis score."""
-    from sfm_amd import ransac, synth
+    """C2 at full size: one KITTI pair, N = 435,032, H = 4096 (ransac_iter 8),
+    on the benched scorer (dispatch asserted).  The default launch
+    (k_score_mf2 with count-bound pruning) and the per-hypothesis-score launch
+    (k_score_mf2, one launch) both give the oracle's winner, count, E and P;
+    the latter also every hypothesis score."""
+    from sfm_amd import _lib, ransac, synth
+    assert _lib.tune_get("score_mf") == 2 and _lib.tune_get("score_mf_prune") > 0
     flow, K, pose, depth = synth.kitti_pair_batch(1, seed=21)
     pts = ransac.flow_to_points(flow.to(cuda), torch.inverse(K).to(cuda))
     E, P, inl, win = ransac.ransac5_batched(pts, None, None, None, 8, 1e-4)
+    assert _lib.last_scorer() == "k_score_mf2+prune"
     E2, P2, inl2, win2, scores = ransac.ransac5_batched(pts, None, None, None, 8, 1e-4, return_scores=True)
+    assert _lib.last_scorer() == "k_score_mf2"
     p = pts[0].cpu().numpy()
     ref = R.ransac5(p[:, :2], p[:, 2:], 435032, 435032, 8, 1e-4, nthreads=16)
     for e, pp, i, w in ((E, P, inl, win), (E2, P2, inl2, win2)):

@@ -26,6 +26,16 @@ from oracle import ransac5 as ORR
 pytestmark = pytest.mark.gpu
 
 
+def _score(data, Et, thr, dev):
+    """Counts through sfm_score_essentials on the benched scorer, pinned:
+    k_score_mf2 in the matrix-core threshold range [2^-15, 1), k_score32 below."""
+    from sfm_amd import _lib, ransac
+    _lib.tune("score_mf", 2)          # restored by conftest's tuning snapshot
+    got = ransac.score_essentials(torch.from_numpy(data).to(dev), torch.from_numpy(Et).to(dev), thr).cpu().numpy()
+    assert _lib.last_scorer() == ("k_score_mf2" if 2.0 ** -15 <= thr < 1.0 else "k_score32"), _lib.last_scorer()
+    return got
+
+
 def _err(E, q, qp):
     """The reference's error in its own operation order (float64, numpy)."""
     x = np.c_[q, np.ones(len(q))]
@@ -120,7 +130,7 @@ def test_decisions_at_the_threshold_and_band_edges(cuda, thr):
         data[bi, :, :2] = q
         data[bi, :, 2:] = pts[nm]
     Et = np.stack([np.stack(Es)] * B)
-    got = ransac.score_essentials(torch.from_numpy(data).to(cuda), torch.from_numpy(Et).to(cuda), thr).cpu().numpy()
+    got = _score(data, Et, thr, cuda)
     for bi, nm in enumerate(names):
         q = np.ascontiguousarray(data[bi, :, :2])
         qp = np.ascontiguousarray(data[bi, :, 2:])
@@ -152,7 +162,7 @@ def test_every_e_on_its_own_band_edge(cuda):
         data[i, n_p:, :2] = q
         data[i, n_p:, 2:] = base + hi[:, None] * nrm
     Et = np.stack([np.stack(Es)] * n_e)
-    got = ransac.score_essentials(torch.from_numpy(data).to(cuda), torch.from_numpy(Et).to(cuda), thr).cpu().numpy()
+    got = _score(data, Et, thr, cuda)
     for i in range(n_e):
         q = np.ascontiguousarray(data[i, :, :2])
         qp = np.ascontiguousarray(data[i, :, 2:])
