@@ -95,6 +95,10 @@ def parse(argv=None):
                     help="launch-shape tuning keys for A/B runs, 'key=value,key=value' (sfm_tune_set; "
                          "include/sfm_hip.h lists them); recorded in config.tune")
     args = ap.parse_args(argv)
+    if args.pipeline and args.overlap_ref != "0":
+        # step_pipelined writes the whole volume and ignores overlap_ref: the
+        # warped-half byte count would misstate the sweep's traffic
+        ap.error("--pipeline and --overlap-ref are exclusive")
     b, hw, it, nl, cd, kp = CONFIGS[args.config]
     args.batch = b if args.batch is None else args.batch
     args.iters = it if args.iters is None else args.iters

@@ -123,6 +123,7 @@ const TuneKey kTuneKeys[] = {
     {"score_prune", &sfm::Tuning::score_prune, v_01},
     {"score_mf", &sfm::Tuning::score_mf, [](int v) { return v >= 0 && v <= 2; }},
     {"score_mf_prune", &sfm::Tuning::score_mf_prune, [](int v) { return v == 0 || (v >= 500 && v <= 990); }},
+    {"score_mf_chunk", &sfm::Tuning::score_mf_chunk, [](int v) { return v >= 1 && v <= 4096; }},
     {"score_mf_blocks_per_cu", &sfm::Tuning::score_mf_blocks_per_cu, [](int v) { return v >= 1 && v <= 8; }},
     {"score_interleave", &sfm::Tuning::score_interleave, v_01},
     {"conv_rolling", &sfm::Tuning::conv_rolling, v_01},

@@ -24,6 +24,7 @@
 // inlier_fast below) and re-evaluates the rare undecided ones in the
 // reference's exact operation order.
 #include <algorithm>
+#include <mutex>
 #include <vector>
 #include "common.h"
 #include "five_point.h"
@@ -1560,15 +1561,15 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
       // count-bound pruning: every candidate on the first prune_pm per mille
       // of each pair's spans, k_mf2_prune, the kept ones on the rest
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)nullptr, 0, prune_pm);
+                         kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, tuning().score_mf_chunk);
       hipLaunchKernelGGL(k_mf2_prune<Src>, dim3(bc), dim3(1024), 0, s, src, pp, cmax, prune_pm, w.cand_total,
                          w.candE, w.cntT, kc, w.cand_live, w.cmap, w.skipped);
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_live, w.candE, w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)w.cmap, prune_pm, 1000);
+                         kc, w.claim, (const int32_t*)w.cmap, prune_pm, 1000, tuning().score_mf_chunk);
       set_last_scorer("k_score_mf2+prune");
     } else if (same && tuning().score_mf == 2) {
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)nullptr, 0, 1000);
+                         kc, w.claim, (const int32_t*)nullptr, 0, 1000, tuning().score_mf_chunk);
       set_last_scorer("k_score_mf2");
     } else if (same) {
       hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
@@ -1630,11 +1631,12 @@ __global__ __launch_bounds__(256) void k_fill_cands(const double* __restrict__ E
 // k_roots with the split isolation (five_point.h, isolate_p1 / falsi_tasks /
 // bisect_deferred): lanes [0, lanes) of each wave own one hypothesis each
 // through phase 1; phases 2 and 3 run over a task list on every lane.  NW = 1
-// (roots_split 1): one wave per block and its own list, so the launch lasts as
-// long as its busiest wave (profiles/r03_roots_split_stats.txt: 245 k cycles
-// per wave on average, 313-325 k at most).  NW = 4 (roots_split 2, default):
-// the block's four waves append to and claim from one pool (LDS counters), so
-// the tail averages over four waves' tasks.  Phase 1 stays per hypothesis, and
+// (roots_split 1, the default): one wave per block and its own list, so the
+// launch lasts as long as its busiest wave (profiles/r03_roots_split_stats.txt:
+// 245 k cycles per wave on average, 313-325 k at most).  NW = 4 (roots_split
+// 2, opt-in): the block's four waves append to and claim from one pool (LDS
+// counters), so the tail averages over four waves' tasks -- measured 2-6 %
+// slower (profiles/r04_roots_pool_ab.txt).  Phase 1 stays per hypothesis, and
 // every node's root goes to its fixed slot: the workspace is byte-identical.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void k_roots_split(int H, int lanes, double* __restrict__ st, size_t stride,
@@ -1699,9 +1701,45 @@ __global__ __launch_bounds__(64 * NW) void k_roots_split(int H, int lanes, doubl
 // Score fence (sfm_score_fence_enable / _wait): an event recorded on the
 // RANSAC stream right before the scoring phase, so that a second stream can
 // start pose-independent memory work (the cost volume's reference half) beside
-// the compute-bound scorer instead of beside the latency-bound solve.
-static hipEvent_t g_score_fence = nullptr;
-static bool g_score_fence_on = false;
+// the compute-bound scorer instead of beside the latency-bound solve.  One
+// event per device, created on that device (the device of the stream it is
+// recorded on / waited from, never the caller's current device); recording is
+// on while any enable(1) is not matched by an enable(0).
+constexpr int kFenceDevices = 64;
+static std::mutex g_fence_mu;
+static hipEvent_t g_fence[kFenceDevices] = {};
+static int g_fence_refs = 0;
+
+static int stream_device(hipStream_t s, int* dev) {
+  if (hipStreamGetDevice(s, dev) != hipSuccess) SFM_HIP(hipGetDevice(dev));
+  SFM_REQUIRE(*dev >= 0 && *dev < kFenceDevices, "score fence: device index out of range");
+  return SFM_OK;
+}
+
+// the fence of the stream's device (created there on first use); g_fence_mu held
+static int fence_of(hipStream_t s, hipEvent_t* ev) {
+  int dev = 0;
+  if (int rc = stream_device(s, &dev)) return rc;
+  if (!g_fence[dev]) {
+    int cur = 0;
+    SFM_HIP(hipGetDevice(&cur));
+    SFM_HIP(hipSetDevice(dev));
+    const hipError_t e = hipEventCreateWithFlags(&g_fence[dev], hipEventDisableTiming);
+    SFM_HIP(hipSetDevice(cur));
+    SFM_HIP(e);
+  }
+  *ev = g_fence[dev];
+  return SFM_OK;
+}
+
+static int record_score_fence(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_fence_mu);
+  if (g_fence_refs <= 0) return SFM_OK;
+  hipEvent_t ev = nullptr;
+  if (int rc = fence_of(s, &ev)) return rc;
+  SFM_HIP(hipEventRecord(ev, s));
+  return SFM_OK;
+}
 
 template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
@@ -1791,7 +1829,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     SFM_HIP(hipMemsetAsync(w.cov, 0, (size_t)bc * cmax * 8, s));
     SFM_HIP(hipMemsetAsync(w.best_lb, 0, SFM_MAX_BATCH * kBestStride * 4, s));
   }
-  if (g_score_fence_on && g_score_fence) SFM_HIP(hipEventRecord(g_score_fence, s));
+  if (int rc = record_score_fence(s)) return rc;
   {
     ProfScope ps("ransac_score", s);
     ScoreBufs sb{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim};
@@ -1922,14 +1960,17 @@ int sfm_ransac5_flow(const float* flow, int batch, int H, int W, int h_side, int
 }
 
 int sfm_score_fence_enable(int on) {
-  if (on && !g_score_fence) SFM_HIP(hipEventCreateWithFlags(&g_score_fence, hipEventDisableTiming));
-  g_score_fence_on = on != 0;
+  std::lock_guard<std::mutex> lk(g_fence_mu);
+  g_fence_refs = on ? g_fence_refs + 1 : std::max(0, g_fence_refs - 1);
   return SFM_OK;
 }
 
 int sfm_score_fence_wait(void* stream) {
-  SFM_REQUIRE(g_score_fence, "score fence not enabled");
-  SFM_HIP(hipStreamWaitEvent((hipStream_t)stream, g_score_fence, 0));
+  std::lock_guard<std::mutex> lk(g_fence_mu);
+  SFM_REQUIRE(g_fence_refs > 0, "score fence not enabled");
+  hipEvent_t ev = nullptr;
+  if (int rc = fence_of((hipStream_t)stream, &ev)) return rc;
+  SFM_HIP(hipStreamWaitEvent((hipStream_t)stream, ev, 0));
   return SFM_OK;
 }
 

@@ -38,7 +38,6 @@ constexpr int kMf2Waves = 12;                  // 3 per SIMD, two accumulator se
 constexpr int kMf2Wpe = kMf2Waves / 4;
 constexpr int kMf2Span = 1024;                 // points per staged span
 constexpr int kMf2Tiles = kMf2Span / 32;       // tiles per span (every run decides all of them)
-constexpr int kMf2MinChunk = 128;              // smallest claimed unit range (candidate tiles)
 constexpr int kMf2Guide = 2;                   // a claim takes remainder / (guide x blocks per XCD)
 constexpr int kMf2Queue = 128;                 // undecided entries per wave and drain window (LDS)
 // candidate tiles the LDS count table holds (tiles past it publish per run)
@@ -158,7 +157,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
     const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
     ScoreConsts kc, unsigned long long* __restrict__ claim, const int32_t* __restrict__ cmap, int sp_lo,
-    int sp_hi) {
+    int sp_hi, int min_chunk) {
   // one count array: this kernel runs only when num_test == num_ransac_test,
   // so the preselection count is the score and k_select reads cntT for both
   __shared__ __attribute__((aligned(16))) _Float16 s_frag[kMf2Tiles][3][64][8];
@@ -208,7 +207,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   // Unit ranges: workgroup ids are dealt round-robin over the 8 XCDs, so
   // id % 8 names the XCD.  XCD x owns the x-th eighth of the units and its
   // blocks claim guided chunks of it from a global counter (half the
-  // remainder's per-block share, at least kMf2MinChunk units); a block whose
+  // remainder's per-block share, at least min_chunk units); a block whose
   // eighth is exhausted takes chunks of the next XCDs' eighths.  Static
   // contiguous ranges left blocks idle for 6 % of the launch on average
   // (round 3): units cost unequal time across pairs and XCDs.
@@ -257,7 +256,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         const long long seg_beg = U * x / nx, seg_end = U * (x + 1) / nx;
         // the floor never exceeds a block's static share of the eighth (small
         // launches, e.g. 2,048 keypoints: a 128-unit floor would idle most blocks)
-        const long long floor_c = max(min((long long)kMf2MinChunk, (seg_end - seg_beg + per_x - 1) / per_x), 1ll);
+        const long long floor_c = max(min((long long)min_chunk, (seg_end - seg_beg + per_x - 1) / per_x), 1ll);
         const long long rem = seg_end - seg_beg - (long long)__hip_atomic_load(claim + x, __ATOMIC_RELAXED,
                                                                                 __HIP_MEMORY_SCOPE_AGENT);
         if (rem <= 0) continue;

@@ -1475,7 +1475,10 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   const int nq = tuning().sweep_group == 8 ? 2 : 1;
   const int64_t slab = (int64_t)L * hw;
   const int fgroups = (C + 4 * nq - 1) / (4 * nq);
-  const int mode = tuning().sweep_flat;
+  // the warped half alone (write_ref = 0): only k_sweep_tile honours write_ref
+  // (the other forms would also write the reference rows, racing the side
+  // stream's k_ref_planes with the same values), so it always takes that form
+  const int mode = write_ref ? tuning().sweep_flat : 2;
   // k_sweep_tile: 256 * nj elements per window (bf16 packs register pairs: nj even)
   int nj = tuning().sweep_nj;
   if (out_dtype == 1 && nj < 2) nj = 2;
@@ -1574,6 +1577,7 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     SFM_LAUNCHED();
     return SFM_OK;
   }
+  SFM_REQUIRE(write_ref, "warped-half sweep: the shape is outside k_sweep_tile's range");
   ProfScope ps(pname, s);
   if (out_dtype == 0) {
     if (vec) launch_k_sweep<float, true>(ipb, blocks, s, ref, tq, pose, K4, K4inv, g, out);
@@ -1773,6 +1777,8 @@ int sfm_plane_sweep_ref_planes(const float* ref, int batch, int channels, int h,
               "invalid sweep shape");
   SFM_REQUIRE(out_dtype == 0 || out_dtype == 1, "out_dtype must be 0 (float32) or 1 (bfloat16)");
   SFM_REQUIRE((int64_t)h * w < ((int64_t)1 << 30), "feature map too large");
+  // k_ref_pad / k_ref_planes_generic take one (pair, channel) row per grid y
+  SFM_REQUIRE((int64_t)batch * channels <= 65535, "batch * channels must be <= 65535");
   hipStream_t s = (hipStream_t)stream;
   const int hw = h * w;
   const int64_t slab = (int64_t)nlabel * hw;

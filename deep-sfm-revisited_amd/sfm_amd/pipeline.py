@@ -77,7 +77,18 @@ class TwoViewHotPath:
         if self.overlap_ref:
             self.ref_ws = sweep.ref_planes_workspace_for(B, self.C, self.h, self.w, self.device)
             self.ref_stream = torch.cuda.Stream(device=self.device)
+            # per-device fence (created on the stream's device), reference-counted:
+            # released in __del__
             _lib.check(_lib.load().sfm_score_fence_enable(1), "sfm_score_fence_enable")
+            self._fence_on = True
+
+    def __del__(self):
+        if getattr(self, "_fence_on", False):
+            self._fence_on = False
+            try:
+                _lib.load().sfm_score_fence_enable(0)
+            except Exception:
+                pass
 
     @staticmethod
     def k_inverse(K):

@@ -257,10 +257,16 @@ int sfm_plane_sweep_psnet(const float* ref, const float* tgt, int batch, int cha
  *       same values).
  * Together they write exactly sfm_plane_sweep_psnet's volume. */
 size_t sfm_plane_sweep_ref_planes_workspace_bytes(int batch, int channels, int h, int w);
-/* Score fence: with it enabled, every RANSAC call records a library-owned
+/* Score fence: while enabled, every RANSAC call records a library-owned
  * event on its stream right before its scoring phase; sfm_score_fence_wait
- * makes `stream` wait for the last one recorded (so the reference half can run
- * beside the compute-bound scorer rather than the latency-bound solve). */
+ * makes `stream` wait for the last one recorded on that stream's device (so
+ * the reference half can run beside the compute-bound scorer rather than the
+ * latency-bound solve).  One event per device, created on the device of the
+ * stream (not the caller's current device).  enable(1) / enable(0) are
+ * reference-counted: recording stays on until every enable(1) has been
+ * matched by an enable(0) (TwoViewHotPath enables it for its lifetime).
+ * Every RANSAC call on a device records the same fence, so two hot paths
+ * sharing a device wait on whichever scoring phase was enqueued last. */
 int sfm_score_fence_enable(int on);
 int sfm_score_fence_wait(void* stream);
 int sfm_plane_sweep_ref_planes(const float* ref, int batch, int channels, int h, int w, int nlabel, int out_dtype,
@@ -414,6 +420,8 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *     "score_mf"              0..2    split-f16 matrix-core scorers (2: span-major
  *                                     k_score_mf2, 1: k_score_mf, 0: VALU scorers;
  *                                     2 by default; exact by proof, same counts)
+ *     "score_mf_chunk"        1..4096 k_score_mf2's smallest claimed unit range, in
+ *                                     (span, 32-candidate tile) units (128)
  *     "score_mf_prune"        0, 500..990  count-bound pruning in k_score_mf2 (900):
  *                                     every candidate scored on the first N per
  *                                     mille of each pair's 1024-point spans, then

@@ -155,7 +155,7 @@ def test_tuning_keys_round_trip():
     block = doc[doc.index("Tuning knobs"):doc.index("int sfm_tune_set")]
     keys = re.findall(r'"([a-z0-9_]+)"', block)
     assert set(keys) == set(_lib.tune_keys())           # documented == exported (sfm_tune_key)
-    assert len(set(keys)) == 25 and "score_mf_prune" in keys and "score_lowp_template" in keys
+    assert len(set(keys)) == 26 and "score_mf_prune" in keys and "score_lowp_template" in keys
     for k in keys:
         _lib.tune_get(k)
     old = _lib.tune_get("sweep_nj")
@@ -186,3 +186,16 @@ def test_profile_select_filters_names():
     _lib.profile_select(None)
     assert _lib.load().sfm_profile_select(b",,ransac_score,") == 0
     _lib.profile_select(None)
+
+
+def test_score_fence_reference_counted():
+    """sfm_score_fence_enable is reference-counted (TwoViewHotPath enables it
+    for its lifetime); waiting with no enable left is refused before any HIP
+    call (CPU-safe)."""
+    from sfm_amd import _lib
+    lib = _lib.load()
+    assert lib.sfm_score_fence_enable(0) == 0            # never below zero
+    assert lib.sfm_score_fence_wait(None) == 1
+    assert lib.sfm_score_fence_enable(1) == 0 and lib.sfm_score_fence_enable(1) == 0
+    assert lib.sfm_score_fence_enable(0) == 0 and lib.sfm_score_fence_enable(0) == 0
+    assert lib.sfm_score_fence_wait(None) == 1 and b"not enabled" in lib.sfm_last_error()

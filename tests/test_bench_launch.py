@@ -8,6 +8,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -200,3 +202,12 @@ def test_tune_option_parses():
     a = bench.parse(["--tune", "sweep_store_px=2,sweep_nj=2", "--config", "c3"])
     assert a.tune == "sweep_store_px=2,sweep_nj=2" and a.config == "c3"
     assert bench.parse([]).tune == ""
+
+
+def test_pipeline_and_overlap_ref_are_exclusive():
+    """step_pipelined writes the whole volume and ignores overlap_ref, so the
+    combination is refused rather than reported with the warped-half bytes."""
+    import bench
+    with pytest.raises(SystemExit):
+        bench.parse(["--pipeline", "--overlap-ref", "score"])
+    assert bench.parse(["--overlap-ref", "score"]).overlap_ref == "score"

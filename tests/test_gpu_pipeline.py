@@ -68,3 +68,50 @@ def test_ref_planes_alone_write_only_the_reference_rows(cuda):
     torch.cuda.synchronize()
     assert torch.equal(out[:, :C], ref.unsqueeze(2).expand(B, C, L, h, w))
     assert bool((out[:, C:] == 7.0).all())
+
+
+def test_score_fence_per_device_and_released(cuda):
+    """The score fence lives on the device of the stream it is recorded on and
+    stays enabled while any overlap_ref hot path lives: a second hot path's
+    release leaves the first one's steps working, and after the last one is
+    gone waiting is refused (reference count back to zero)."""
+    import gc
+    from sfm_amd import _lib, synth
+    from sfm_amd.pipeline import TwoViewHotPath
+    B, C, L, fhw = 1, 32, 8, (20, 30)
+    flow, K, _, _ = synth.kitti_pair_batch(B, seed=31, hw=(120, 200), device=cuda)
+    ref, tgt = synth.features(B, C, *fhw, seed=31, device=cuda)
+    mk = lambda ov: TwoViewHotPath(B, (120, 200), fhw, C, L, 2, 1e-3, 1.0, True, 0.6, device=cuda, overlap_ref=ov)
+    gc.collect()
+    before = _lib.load().sfm_score_fence_wait(_lib.stream_ptr(cuda))   # 1 unless an earlier hot path still lives
+    a, b = mk("score"), mk("score")
+    del b
+    gc.collect()
+    plain = mk(False)
+    E2, P2, i2, c2 = a.step(flow, K, ref, tgt)
+    E1, P1, i1, c1 = plain.step(flow, K, ref, tgt)
+    torch.cuda.synchronize()
+    assert torch.equal(c1, c2) and torch.equal(E1, E2)
+    del a
+    gc.collect()
+    assert _lib.load().sfm_score_fence_wait(_lib.stream_ptr(cuda)) == before
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2, reason="needs two GPUs")
+def test_overlap_hot_path_on_non_current_device():
+    """a hot path built for a device other than the current one
+    records and waits on that device's own fence."""
+    from sfm_amd import synth
+    from sfm_amd.pipeline import TwoViewHotPath
+    dev = torch.device("cuda", 1)
+    torch.cuda.set_device(0)
+    B, C, L, fhw = 1, 32, 8, (20, 30)
+    flow, K, _, _ = synth.kitti_pair_batch(B, seed=32, hw=(120, 200), device=dev)
+    ref, tgt = synth.features(B, C, *fhw, seed=32, device=dev)
+    over = TwoViewHotPath(B, (120, 200), fhw, C, L, 2, 1e-3, 1.0, True, 0.6, device=dev, overlap_ref="score")
+    plain = TwoViewHotPath(B, (120, 200), fhw, C, L, 2, 1e-3, 1.0, True, 0.6, device=dev)
+    with torch.cuda.device(dev):
+        c2 = over.step(flow, K, ref, tgt)[3]
+        c1 = plain.step(flow, K, ref, tgt)[3]
+        torch.cuda.synchronize(dev)
+    assert torch.equal(c1, c2)
