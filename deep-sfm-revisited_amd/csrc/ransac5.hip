@@ -72,8 +72,8 @@ struct Workspace {
   int32_t* best_lb;             // [64] largest partial count seen (a lower bound on the winning score)
   unsigned long long* skipped;  // [1] evaluations skipped by pruning (whole call)
   unsigned long long* claim;    // [9] k_score_mf2's range-claim counters and finished-block count (zero between launches)
-  int32_t* cmap;       // [B][Cmax] k_mf2_prune: the kept candidates of each pair, in order
-  int32_t* cand_live;  // [64] k_mf2_prune: kept candidates per pair
+  int32_t* cmap;       // [B][Cmax] k_mf2_keep: the kept candidates of each pair
+  int32_t* lead;       // [4][64] k_mf2_lead / _keep: leader count, index, rest count, kept candidates
   double* pack;        // [n_max][4] (last: its size is the only n_max-dependent one)
 };
 
@@ -106,7 +106,7 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   // field it uses must sit at an offset independent of n_max
   t.claim = (unsigned long long*)take(kMf2ClaimBytes);
   t.cmap = (int32_t*)take(bc * C * 4);
-  t.cand_live = (int32_t*)take(SFM_MAX_BATCH * 4);
+  t.lead = (int32_t*)take(SFM_MAX_BATCH * 4 * 4);
   t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
   if (w) *w = t;
   return off;
@@ -1536,8 +1536,8 @@ struct ScoreBufs {
   int32_t* cntT;
   int32_t* cntR;
   unsigned long long* claim;   // [9] k_score_mf2's range-claim counters and finished-block count
-  int32_t* cmap = nullptr;     // count-bound pruning (k_mf2_prune): kept candidates, their number,
-  int32_t* cand_live = nullptr;   // the evaluations skipped
+  int32_t* cmap = nullptr;     // count-bound pruning (k_mf2_lead / _keep): kept candidates, the
+  int32_t* lead = nullptr;     // leader records (their [3] = kept candidates), the evaluations skipped
   unsigned long long* skipped = nullptr;
 };
 
@@ -1554,17 +1554,20 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
                            bool fast32, int cus, int grid, hipStream_t s, int prune_pm = 0) {
   if (use_mf) {
     hipLaunchKernelGGL(k_mf_cands, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax, w.cand_total, w.candE,
-                       w.candF, mp, w.claim);
+                       w.candF, mp, w.claim, prune_pm > 0 ? w.lead : nullptr);
     const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
     const dim3 g2(std::max(1, cus)), b2(kMf2Waves * 64);
     if (same && tuning().score_mf == 2 && prune_pm > 0) {
       // count-bound pruning: every candidate on the first prune_pm per mille
-      // of each pair's spans, k_mf2_prune, the kept ones on the rest
+      // of each pair's spans, k_mf2_lead + k_mf2_keep, the kept ones on the rest
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
                          kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, tuning().score_mf_chunk);
-      hipLaunchKernelGGL(k_mf2_prune<Src>, dim3(bc), dim3(1024), 0, s, src, pp, cmax, prune_pm, w.cand_total,
-                         w.candE, w.cntT, kc, w.cand_live, w.cmap, w.skipped);
-      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_live, w.candE, w.candF, w.cntT,
+      hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax, prune_pm,
+                         w.cand_total, w.candE, w.cntT, kc, w.lead);
+      hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax, prune_pm,
+                         w.cand_total, w.cntT, w.lead, w.cmap, w.skipped);
+      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH, w.candE,
+                         w.candF, w.cntT,
                          kc, w.claim, (const int32_t*)w.cmap, prune_pm, 1000, tuning().score_mf_chunk);
       set_last_scorer("k_score_mf2+prune");
     } else if (same && tuning().score_mf == 2) {
@@ -1816,7 +1819,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
   MfParams mp{};
   const bool use_mf = fast32 && tuning().score_mf && mf_params(thr, &mp);
   kc.prune = (fast32 && !use_mf && same && !score_out && tuning().score_prune) ? 1 : 0;
-  // count-bound pruning in k_score_mf2 (k_mf2_prune): same condition, and
+  // count-bound pruning in k_score_mf2 (k_mf2_lead / _keep): same condition, and
   // every pair long enough that the second launch has spans to skip
   int min_spans = INT32_MAX;
   for (int b = 0; b < bc; ++b) min_spans = std::min(min_spans, mf2_spans(std::max(pp.test[b], pp.rtest[b])));
@@ -1834,7 +1837,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     ProfScope ps("ransac_score", s);
     ScoreBufs sb{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim};
     sb.cmap = w.cmap;
-    sb.cand_live = w.cand_live;
+    sb.lead = w.lead;
     sb.skipped = w.skipped;
     score_dispatch(src, pp, bc, cmax, sb, kc, mp, use_mf, same, prec, fast, fast32, cus, grid, s, mf2_pm);
   }

@@ -163,12 +163,16 @@ __device__ __forceinline__ _Float16 f16_upf(float v) {
 
 // One thread per candidate: the four A rows of its record.
 __global__ void k_mf_cands(int cmax, const int32_t* __restrict__ cand_total, const double* __restrict__ candE,
-                           _Float16* __restrict__ candF, MfParams mp, unsigned long long* __restrict__ claim) {
+                           _Float16* __restrict__ candF, MfParams mp, unsigned long long* __restrict__ claim,
+                           int32_t* __restrict__ lead) {
   const int b = blockIdx.y;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   // k_score_mf2's range-claim counters (one per XCD) and its finished-block
-  // count start every launch at 0
+  // count start every launch at 0, and so do k_mf2_lead's rest counts and
+  // k_mf2_keep's kept counts (lead[128 .. 256))
   if (claim && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 9) claim[threadIdx.x] = 0ull;
+  if (lead && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * SFM_MAX_BATCH)
+    lead[2 * SFM_MAX_BATCH + threadIdx.x] = 0;
   if (c >= cand_total[b]) return;
   const double* E = candE + ((size_t)b * cmax + c) * kCandStride;
   _Float16 row[kMfRec];

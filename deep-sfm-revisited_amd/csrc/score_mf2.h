@@ -28,7 +28,7 @@
 // Count-bound pruning (round 5, tuning key score_mf_prune): the launch can
 // cover only a range of each pair's spans (sp_lo .. sp_hi, in per-mille of
 // the span count), and the candidates can be a compacted subset whose counts
-// go to cntT[cmap[j]] (k_mf2_prune below).
+// go to cntT[cmap[j]] (k_mf2_lead / k_mf2_keep below).
 //
 // Registers (gfx950, 3 waves per SIMD = 168 VGPRs): 2 x 48 accumulators + 16
 // A + 12 B + 32 decision strings in the loop.  The round 2-4 schedule and
@@ -49,7 +49,7 @@ static_assert(kMf2Span <= 1024, "16-bit table counts");
 static_assert(kMf2Tiles <= 32 && kMf2Tiles % 2 == 0, "32-bit decision strings, tiles in pairs");
 
 // the first span of a launch's range: spans * pm / 1000 (k_score_mf2 and
-// k_mf2_prune agree on it)
+// k_mf2_lead / k_mf2_keep agree on it)
 __host__ __device__ inline int mf2_span_at(int spans, int pm) { return (int)(((long long)spans * pm) / 1000); }
 __host__ __device__ inline int mf2_spans(int points) { return (points + kMf2Span - 1) / kMf2Span; }
 
@@ -431,37 +431,52 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 // Count-bound pruning between two k_score_mf2 launches (tuning key
 // score_mf_prune = pm; only for SFMnet's num_test == num_ransac_test without
 // per-hypothesis scores).  The first launch scores every candidate of pair b
-// on its first n1 points (spans [0, spans * pm / 1000)); this kernel, one
-// block per pair:
-//   1. takes the leader: the first candidate with the largest partial count;
-//   2. counts the leader's inliers on the remaining points [n1, M) with the
-//      exact float64 test (inlier_f64v, the drain's): lb = its final count,
-//      a lower bound on the pair's winning count;
-//   3. keeps candidate c iff its bound (M - n1) + count(c) -- every point not
-//      yet scored an inlier -- is >= lb, and writes the kept candidates'
-//      indices in order (cmap) and their number (cand_live).
+// on its first n1 points (spans [0, spans * pm / 1000)); then
+//   k_mf2_lead  (kLeadBlocks blocks per pair) takes the leader, the first
+//               candidate with the largest partial count, and counts its
+//               inliers on the remaining points [n1, M) with the exact
+//               float64 test (inlier_f64v, the drain's), each block a slice:
+//               lb = partial + rest is the leader's final count, a lower
+//               bound on the pair's winning count;
+//   k_mf2_keep  (one block per 1024 candidates) keeps candidate c iff its
+//               bound (M - n1) + count(c) -- every point not yet scored an
+//               inlier -- is >= lb, appending the kept indices to cmap
+//               (in order within a block; blocks in arrival order).
 // The second launch scores the kept candidates on the remaining spans.  A
 // dropped candidate's true count is < lb <= the winning count, so it can be
 // neither a winner nor tie one: every candidate that reaches the winning
 // count is kept and counted exactly, and k_select's first-max choices
-// (within each hypothesis, then over hypotheses) are unchanged.  The counts
-// of dropped candidates stay partial (lower than their true counts), which is
-// why pruning is off when per-hypothesis scores are requested.  `skipped`
-// gains (dropped candidates) x (M - n1) evaluations.
+// (within each hypothesis, then over hypotheses) are unchanged.  (The order
+// of cmap only decides which kept candidates share a tile; every count is
+// exact either way.)  The counts of dropped candidates stay partial (lower
+// than their true counts), which is why pruning is off when per-hypothesis
+// scores are requested.  `skipped` gains (dropped candidates) x (M - n1).
+// lead[k * SFM_MAX_BATCH + b], k = 0: partial count of the leader, 1: its
+// index, 2: its rest count, 3: kept candidates (the second launch's
+// cand_total); 2 and 3 are zeroed by k_mf_cands at the start of the scoring
+// phase.
+constexpr int kLeadBlocks = 32;
+
+__device__ __forceinline__ int mf2_n1(const PairParams& pp, int b, int pm) {
+  const int M = max(pp.test[b], pp.rtest[b]);
+  return min(mf2_span_at(mf2_spans(M), pm) * kMf2Span, M);
+}
+
 template <class Src>
-__global__ __launch_bounds__(1024) void k_mf2_prune(const Src src, PairParams pp, int cmax, int pm,
-                                                   const int32_t* __restrict__ cand_total,
-                                                   const double* __restrict__ candE, const int32_t* __restrict__ cntT,
-                                                   ScoreConsts kc, int32_t* __restrict__ cand_live,
-                                                   int32_t* __restrict__ cmap, unsigned long long* __restrict__ skipped) {
+__global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp, int cmax, int pm,
+                                                  const int32_t* __restrict__ cand_total,
+                                                  const double* __restrict__ candE, const int32_t* __restrict__ cntT,
+                                                  ScoreConsts kc, int32_t* __restrict__ lead) {
   __shared__ unsigned long long s_key[16];
   __shared__ int s_part[16];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int M = max(pp.test[b], pp.rtest[b]);
-  const int n1 = min(mf2_span_at(mf2_spans(M), pm) * kMf2Span, M);
+  const int n1 = mf2_n1(pp, b, pm);
   const int ctot = cand_total[b];
+  if (ctot <= 0) return;
   const int32_t* cnt = cntT + (size_t)b * cmax;
-  // 1. the leader (key count << 32 | ~c: the first of the largest)
+  // the leader (key count << 32 | ~c: the first of the largest); every block
+  // finds the same one
   unsigned long long key = 0ull;
   for (int c = tid; c < ctot; c += 1024) {
     const unsigned long long k = ((unsigned long long)(uint32_t)cnt[c] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)c);
@@ -476,41 +491,59 @@ __global__ __launch_bounds__(1024) void k_mf2_prune(const Src src, PairParams pp
   __syncthreads();
   key = s_key[0];
   for (int w = 1; w < 16; ++w) key = s_key[w] > key ? s_key[w] : key;
-  if (ctot <= 0) {
-    if (tid == 0) cand_live[b] = 0;
-    return;
-  }
-  const int lead = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
-  // 2. its exact count on the points the first launch did not score
-  const double* El = candE + ((size_t)b * cmax + lead) * kCandStride;
+  const int ld = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
+  // this block's slice of the points the first launch did not score
+  const int rest_n = M - n1;
+  const int k0 = n1 + (int)((long long)rest_n * blockIdx.x / gridDim.x);
+  const int k1 = n1 + (int)((long long)rest_n * (blockIdx.x + 1) / gridDim.x);
+  const double* El = candE + ((size_t)b * cmax + ld) * kCandStride;
   int rest = 0;
-  for (int k = n1 + tid; k < M; k += 1024) rest += inlier_f64v(El, src.load(b, k), kc) ? 1 : 0;
+  for (int k = k0 + tid; k < k1; k += 1024) rest += inlier_f64v(El, src.load(b, k), kc) ? 1 : 0;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) rest += __shfl_xor(rest, d, 64);
-  __syncthreads();                                           // s_part reuse below
   if (lane == 0) s_part[wv] = rest;
   __syncthreads();
-  rest = 0;
-  for (int w = 0; w < 16; ++w) rest += s_part[w];
-  const long long lb = (long long)(key >> 32) + rest;
-  // 3. the kept candidates, compacted in order
-  int base = 0;
-  int32_t* map = cmap + (size_t)b * cmax;
-  for (int c0 = 0; c0 < ctot; c0 += 1024) {
-    const int c = c0 + tid;
-    const bool keep = c < ctot && (long long)(M - n1) + cnt[c] >= lb;
-    const unsigned long long bal = __ballot(keep);
-    const int below = __popcll(bal & ((1ull << lane) - 1ull));
-    __syncthreads();                                         // the previous round's s_part reads are done
-    if (lane == 0) s_part[wv] = __popcll(bal);
-    __syncthreads();
-    int off = base;
-    for (int w = 0; w < wv; ++w) off += s_part[w];
-    if (keep) map[off + below] = c;
-    for (int w = 0; w < 16; ++w) base += s_part[w];
-  }
   if (tid == 0) {
-    cand_live[b] = base;
-    if (skipped) atomicAdd(skipped, (unsigned long long)(ctot - base) * (unsigned long long)(M - n1));
+    int r = 0;
+    for (int w = 0; w < 16; ++w) r += s_part[w];
+    if (blockIdx.x == 0) {
+      lead[0 * SFM_MAX_BATCH + b] = (int)(key >> 32);
+      lead[1 * SFM_MAX_BATCH + b] = ld;
+    }
+    if (r) atomicAdd(&lead[2 * SFM_MAX_BATCH + b], r);
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, int pm,
+                                                  const int32_t* __restrict__ cand_total,
+                                                  const int32_t* __restrict__ cntT, int32_t* __restrict__ lead,
+                                                  int32_t* __restrict__ cmap, unsigned long long* __restrict__ skipped) {
+  __shared__ int s_part[16];
+  __shared__ int s_base;
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ctot = cand_total[b];
+  const int c0 = blockIdx.x * 1024;
+  if (c0 >= ctot) return;
+  const int M = max(pp.test[b], pp.rtest[b]);
+  const int n1 = mf2_n1(pp, b, pm);
+  const long long lb = (long long)lead[0 * SFM_MAX_BATCH + b] + lead[2 * SFM_MAX_BATCH + b];
+  const int c = c0 + tid;
+  const bool keep = c < ctot && (long long)(M - n1) + cntT[(size_t)b * cmax + c] >= lb;
+  const unsigned long long bal = __ballot(keep);
+  if (lane == 0) s_part[wv] = __popcll(bal);
+  __syncthreads();
+  if (tid == 0) {
+    int tot = 0;
+    for (int w = 0; w < 16; ++w) tot += s_part[w];
+    s_base = tot ? atomicAdd(&lead[3 * SFM_MAX_BATCH + b], tot) : 0;
+    const int live = min(1024, ctot - c0);
+    if (skipped && live > tot)
+      atomicAdd(skipped, (unsigned long long)(live - tot) * (unsigned long long)(M - n1));
+  }
+  __syncthreads();
+  if (keep) {
+    int off = s_base + __popcll(bal & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wv; ++w) off += s_part[w];
+    cmap[(size_t)b * cmax + off] = c;
   }
 }

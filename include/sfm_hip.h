@@ -421,12 +421,12 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     k_score_mf2, 1: k_score_mf, 0: VALU scorers;
  *                                     2 by default; exact by proof, same counts)
  *     "score_mf_chunk"        1..4096 k_score_mf2's smallest claimed unit range, in
- *                                     (span, 32-candidate tile) units (128)
- *     "score_mf_prune"        0, 500..990  count-bound pruning in k_score_mf2 (900):
+ *                                     (span, 32-candidate tile) units (64)
+ *     "score_mf_prune"        0, 500..990  count-bound pruning in k_score_mf2 (880):
  *                                     every candidate scored on the first N per
  *                                     mille of each pair's 1024-point spans, then
  *                                     only candidates whose bound can still reach
- *                                     the leader's exact count (k_mf2_prune); 0 =
+ *                                     the leader's exact count (k_mf2_lead / _keep); 0 =
  *                                     one launch.  Winner, count, E, P unchanged;
  *                                     only with num_test == num_ransac_test, no
  *                                     per-hypothesis scores, >= 32 spans per pair
@@ -467,7 +467,7 @@ const char* sfm_tune_key(int index);
 /* The score kernel the most recent RANSAC / score call of this process
  * dispatched ("k_score_mf2", "k_score_mf", "k_score32", ...; "" before any),
  * followed by "+prune" when k_score_mf2 ran with count-bound pruning (two
- * launches and k_mf2_prune between them).  A dispatch check for tests. */
+ * launches and k_mf2_lead / k_mf2_keep between them).  A dispatch check for tests. */
 const char* sfm_last_scorer(void);
 
 /* ------------------------------------------------------------------------
