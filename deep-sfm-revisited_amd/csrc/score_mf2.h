@@ -440,21 +440,20 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 //               bound on the pair's winning count;
 //   k_mf2_keep  (one block per 1024 candidates) keeps candidate c iff its
 //               bound (M - n1) + count(c) -- every point not yet scored an
-//               inlier -- is >= lb, appending the kept indices to cmap
-//               (in order within a block; blocks in arrival order).
+//               inlier -- is >= lb, writing the kept indices to cmap in
+//               candidate order (each block counts the kept candidates
+//               before its own range for its offset).
 // The second launch scores the kept candidates on the remaining spans.  A
 // dropped candidate's true count is < lb <= the winning count, so it can be
 // neither a winner nor tie one: every candidate that reaches the winning
 // count is kept and counted exactly, and k_select's first-max choices
-// (within each hypothesis, then over hypotheses) are unchanged.  (The order
-// of cmap only decides which kept candidates share a tile; every count is
-// exact either way.)  The counts of dropped candidates stay partial (lower
+// (within each hypothesis, then over hypotheses) are unchanged.  The counts
+// of dropped candidates stay partial (lower
 // than their true counts), which is why pruning is off when per-hypothesis
 // scores are requested.  `skipped` gains (dropped candidates) x (M - n1).
 // lead[k * SFM_MAX_BATCH + b], k = 0: partial count of the leader, 1: its
-// index, 2: its rest count, 3: kept candidates (the second launch's
-// cand_total); 2 and 3 are zeroed by k_mf_cands at the start of the scoring
-// phase.
+// index, 2: its rest count (zeroed by k_mf_cands at the start of the scoring
+// phase), 3: kept candidates (the second launch's cand_total).
 constexpr int kLeadBlocks = 32;
 
 __device__ __forceinline__ int mf2_n1(const PairParams& pp, int b, int pm) {
@@ -519,7 +518,7 @@ __global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, int 
                                                   const int32_t* __restrict__ cntT, int32_t* __restrict__ lead,
                                                   int32_t* __restrict__ cmap, unsigned long long* __restrict__ skipped) {
   __shared__ int s_part[16];
-  __shared__ int s_base;
+  __shared__ int s_before[16];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ctot = cand_total[b];
   const int c0 = blockIdx.x * 1024;
@@ -527,23 +526,36 @@ __global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, int 
   const int M = max(pp.test[b], pp.rtest[b]);
   const int n1 = mf2_n1(pp, b, pm);
   const long long lb = (long long)lead[0 * SFM_MAX_BATCH + b] + lead[2 * SFM_MAX_BATCH + b];
+  const int32_t* cnt = cntT + (size_t)b * cmax;
+  auto kept = [&](int c) { return (long long)(M - n1) + cnt[c] >= lb; };
+  // this block's offset: the kept candidates before c0, counted here (a
+  // deterministic order, so the workspace holds no schedule-dependent bytes)
+  int before = 0;
+  for (int c = tid; c < c0; c += 1024) before += kept(c) ? 1 : 0;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) before += __shfl_xor(before, d, 64);
   const int c = c0 + tid;
-  const bool keep = c < ctot && (long long)(M - n1) + cntT[(size_t)b * cmax + c] >= lb;
+  const bool keep = c < ctot && kept(c);
   const unsigned long long bal = __ballot(keep);
-  if (lane == 0) s_part[wv] = __popcll(bal);
+  if (lane == 0) {
+    s_part[wv] = __popcll(bal);
+    s_before[wv] = before;
+  }
   __syncthreads();
+  int base = 0, tot = 0;
+  for (int w = 0; w < 16; ++w) {
+    base += s_before[w];
+    tot += s_part[w];
+  }
+  if (keep) {
+    int off = base + __popcll(bal & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wv; ++w) off += s_part[w];
+    cmap[(size_t)b * cmax + off] = c;
+  }
   if (tid == 0) {
-    int tot = 0;
-    for (int w = 0; w < 16; ++w) tot += s_part[w];
-    s_base = tot ? atomicAdd(&lead[3 * SFM_MAX_BATCH + b], tot) : 0;
+    if (c0 + 1024 >= ctot) lead[3 * SFM_MAX_BATCH + b] = base + tot;   // the last block: the kept count
     const int live = min(1024, ctot - c0);
     if (skipped && live > tot)
       atomicAdd(skipped, (unsigned long long)(live - tot) * (unsigned long long)(M - n1));
-  }
-  __syncthreads();
-  if (keep) {
-    int off = s_base + __popcll(bal & ((1ull << lane) - 1ull));
-    for (int w = 0; w < wv; ++w) off += s_part[w];
-    cmap[(size_t)b * cmax + off] = c;
   }
 }
