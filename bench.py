@@ -511,7 +511,7 @@ def _main_gpu(args, dist):
     torch.cuda.synchronize(dev)
     # HIP events inside the timed region only around the two roofline kernels:
     # every evented launch adds two event records to the stream (sparse step
-    # 1.722 -> 1.772 ms with all seven regions evented, scripts/event_ab.py)
+    # 1.722 -> 1.772 ms with all seven regions evented, git-history scripts/event_ab.py)
     _lib.profile_reset()
     _lib.profile_select(ROOFLINE_REGIONS)
     _lib.profile_enable(True)

@@ -23,7 +23,8 @@ struct Tuning {
   int sweep_buffer = 1;          // k_sweep_tile: buffer-addressed fast path for interior full-group windows
   int sweep_share = 0;           // k_sweep_tile fast path: right-hand taps from the next lane's left-hand taps (DPP)
   int sweep_store_px = -1;       // k_sweep_tile fast path: 16-byte lane stores via LDS, 1/2/4/8 pixels per lane; 0: plain; -1: bf16 2, fp32 plain
-  int sweep_store_nt = 2;        // k_sweep_tile fast path: volume stores with sc0 nt (streaming); 2: bf16 volumes only
+  int sweep_store_nt = 2;        // k_sweep_tile fast path: volume stores with sc0 nt (streaming); 2: bf16 volumes and
+                                 // fp32 volumes of slabs <= 6 MiB (measured by shape)
   int sweep_run = 16;            // k_sweep_band (sweep_flat = 3): planes per block
   int sweep_band_rows = 16;      // k_sweep_band: most target rows staged in LDS (further clipped to 80 KB)
   int score_blocks_per_cu = 32;  // persistent score grid

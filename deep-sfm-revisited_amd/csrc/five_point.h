@@ -358,7 +358,7 @@ __device__ __forceinline__ void reduce_equations(Eqs& A) {
 // Cooperative reduction: one DPP quad (4 lanes) per hypothesis
 // ---------------------------------------------------------------------------
 // With one lane per hypothesis the reduction was 54 % of k_solve_front's
-// cycles (scripts/front_stats.py): dependent LDS round trips and divisions on
+// cycles (git-history scripts/front_stats.py): dependent LDS round trips and divisions on
 // waves with 16 of 64 lanes active.  Here the quad holds the ten rows'
 // 20-column vector in registers, lane s the columns k = s + 4m (m < 5):
 //   k 0..9 -> e0[.][k], 10..15 -> e1[.][k-10], 16..18 -> e2[.][k-16], 19 -> e3[.][0]
@@ -834,7 +834,7 @@ __device__ __forceinline__ void sign_step(const SturmR& S, double a, double& lf,
 }
 
 #ifdef SFM_ROOTS_STATS
-// experiment builds only (scripts/roots_stats.py): Sturm-sequence evaluations
+// experiment builds only (git-history scripts/roots_stats.py): Sturm-sequence evaluations
 // and falsi steps per k_roots thread, indexed by (block, thread)
 __device__ unsigned int g_roots_evals[1 << 17];
 __device__ unsigned int g_roots_falsi[1 << 17];
@@ -1062,7 +1062,7 @@ __device__ __forceinline__ void isolate_r(const SturmR& S, double lo, double hi,
 // and end-point evaluations), bisections and regula-falsi steps in one loop,
 // so every pass pays for all of them whenever any lane of the wave is in each
 // mode, and a wave lasts as long as its busiest hypothesis (p50 11 Sturm
-// evaluations + 38 falsi steps, p99 89 + 70: scripts/roots_stats.py).  What
+// evaluations + 38 falsi steps, p99 89 + 70: git-history scripts/roots_stats.py).  What
 // happens to an isolated single-root interval depends on nothing but the
 // interval, its sign-change count and the sequence, and its root lands at a
 // fixed slot (ioff), so the work is split in phases:
@@ -1075,7 +1075,7 @@ __device__ __forceinline__ void isolate_r(const SturmR& S, double lo, double hi,
 //      own ends (a ballot and a prefix count, no atomics): the ~77 tasks of a
 //      32-hypothesis wave spread over 64 lanes;
 //   3. a node where modrf fails (end points of equal sign: 20 % of the
-//      hypotheses have one, scripts/roots_split_stats.py) or gives up (its
+//      hypotheses have one, git-history scripts/roots_split_stats.py) or gives up (its
 //      iteration limit) goes back to its hypothesis lane, which holds the
 //      Sturm sequence in registers, for sbisect's bisection.
 // Every node sees exactly the reference's operations in their order, and

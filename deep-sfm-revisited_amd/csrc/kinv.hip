@@ -4,7 +4,7 @@
 // takes intrinsic_inv_gpu = torch.inverse(intrinsic_gpu) (models/SFMnet.py:104).
 //
 // The operation order is rocsolver's getrf + getrs as torch drives them, found
-// by scripts/probe_kinv.hip (64 candidate orders against inv_ex on 20,000
+// by git-history scripts/probe_kinv.hip (64 candidate orders against inv_ex on 20,000
 // intrinsic and 20,000 general matrices; one matched every value): the
 // row-major buffer is factored as its transpose M = A^T by LU with partial
 // pivoting (first maximum |m|, whole rows swapped), multipliers m * (1 / pivot),

@@ -972,14 +972,14 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(const Src src, PairPara
 // Only float32 copies of the points stay in registers.  (Plain v_fma_f32
 // issues at twice the fp64 rate on gfx950; packed v_pk_fma_f32 measured no
 // faster.)  The kernel sits at the measured VALU issue ceiling
-// (scripts/probe_vgpr_bank.hip: ~1.15-1.3 ns per wave-FMA per SIMD at 4-8
+// (git-history scripts/probe_vgpr_bank.hip: ~1.15-1.3 ns per wave-FMA per SIMD at 4-8
 // waves), so its cost is its VALU count: 21 per evaluation in the common
 // path.  Undecided evaluations and lanes with a coordinate beyond 2^12 are
 // queued and re-tested in float64.
 // ---------------------------------------------------------------------------
 
 #ifdef SFM_SCORE_STATS
-// experiment builds only (scripts/score_experiment.py): (candidate, point
+// experiment builds only (git-history scripts/score_experiment.py): (candidate, point
 // slot) wave iterations, those with an undecided lane, undecided evaluations
 __device__ unsigned long long g_score_stats[3];
 extern "C" int sfm_experiment_score_stats(unsigned long long* out3) {

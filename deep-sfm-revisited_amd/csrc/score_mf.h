@@ -40,7 +40,7 @@
 //     n 2u max|op| + 2u |result| <= 36u (|C| + sum|ab|).  The bound used is
 //     K_acc = SFM_MF_ACC_U u with SFM_MF_ACC_U = 36 (the larger; the
 //     round-2 build used 16, above the 7.95u measured by
-//     scripts/probe_mfma_f16.hip but not derived): K_acc S (1 + 2^-9) for the
+//     git-history scripts/probe_mfma_f16.hip but not derived): K_acc S (1 + 2^-9) for the
 //     hi x hi MFMA, K_acc (|a| + 2^-8 S) for the second.
 //   * the reference's own float64 rounding: 2^-46 S absolute, 2^-40 relative.
 //   => |a'_computed - a'| <= alpha = aS * |c|_1 M^2 + ... + K_acc |a'|; the
@@ -77,7 +77,7 @@ static_assert(SFM_MF_ACC_U <= 64, "the relative part K_acc |a'| must stay below 
 // eps2 > alpha^2 for delta <= 1/2).  delta trades the relative band (t_lo,
 // t_hi) against the alpha^2 terms; at the bench threshold 1e-4 the alpha^2
 // terms dominate and delta = 2^-5 minimises the undecided band
-// (scripts/band_width_model.py: 0.193 % at 2^-6, 0.145 % at 2^-5, 0.146 % at 2^-4).
+// (git-history scripts/band_width_model.py: 0.193 % at 2^-6, 0.145 % at 2^-5, 0.146 % at 2^-4).
 #ifndef SFM_MF_AMGM
 #define SFM_MF_AMGM 5
 #endif
@@ -386,7 +386,7 @@ __device__ __forceinline__ void mf_drain(const double* __restrict__ sE, const do
 }
 
 #ifdef SFM_MF_STAMPS
-// experiment builds only (scripts/mf_stamps.py): per-phase wave cycles of
+// experiment builds only (git-history scripts/mf_stamps.py): per-phase wave cycles of
 // k_score_mf: [0] item setup + staging, [1] tile loop, [2] queue build,
 // [3] float64 drain, [4] count reduction + atomics, [5] block barrier,
 // [6] next-item prefetch issue; [7] items (vector atomics only)

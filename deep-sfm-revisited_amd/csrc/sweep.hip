@@ -26,7 +26,7 @@ namespace sfm {
 // plane, then row / quad, then pair) and each block takes `ipb` consecutive
 // items, so the resident blocks sweep one contiguous window of the volume.
 // MI355X write bandwidth drops with the number of interleaved store streams
-// (scripts/probe_store_bw.hip: 1 stream 4.9 TB/s, 2 -> 4.5, 4 -> 4.0, many
+// (git-history scripts/probe_store_bw.hip: 1 stream 4.9 TB/s, 2 -> 4.5, 4 -> 4.0, many
 // scattered row chunks -> 3.7): the copy half therefore runs as a single
 // stream, the warped half as 4 (the price of sharing the taps; one row per
 // item would need ~45 VALU ops and 5 vector loads per output element).
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep(const float* __restrict__ 
 // the full volume, the G reference rows of the same channels.  Window starts
 // are 256-byte aligned in absolute address (a window may straddle two
 // planes), so every wave store is one aligned 256-byte segment.
-//   * scripts/probe_store_bw2.hip (profiles/r01_probe_store_bw2.txt): stores
+//   * git-history scripts/probe_store_bw2.hip (profiles/r01_probe_store_bw2.txt): stores
 //     of this shape run at 6.3-7.0 TB/s on MI355X for 1-8 rows per item, the
 //     per-row windows above at 4.0-5.0 (their 256-byte wave segments straddle
 //     cache lines: rows start at arbitrary 4-byte offsets).
@@ -978,6 +978,19 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
     // 4-byte writes gave wrong words at upper-half chunk starts on gfx950 --
     // scripts/diag_wide.py; the cause was not isolated)
     auto put = [&](int slot, const float* v) {
+#ifdef SFM_SWEEP_PAIRSTAGE
+      // experiment builds only (round 5, the round-4 miscompute): the plain
+      // path's DPP-packed bf16 pairs staged as 4-byte LDS writes
+      if constexpr (BF) {
+        uint32_t* st32 = s_rows[wave][slot];
+#pragma unroll
+        for (int s = 0; s < NJ / 2; ++s) {
+          const unsigned u = bf16_pair_swap(to_bf16(v[2 * s]), to_bf16(v[2 * s + 1]), odd);
+          st32[(128 * s + lane + (odd ? 63 : 0)) >> 1] = u;
+        }
+        return;
+      }
+#endif
       OutT* st = reinterpret_cast<OutT*>(s_rows[wave][slot]);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -988,7 +1001,17 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
     auto flush = [&](unsigned r0) {             // rows r0 .. r0 + RPS - 1
       sweep_wave_sync();
       const u32x4 x = *reinterpret_cast<const u32x4*>(&s_rows[wave][rr][4 * cl]);
+#ifdef SFM_SWEEP_STORE_NOP
+      // experiment builds only: the store and one wait state as one asm block
+      if (NT)
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen sc0 nt\n\ts_nop 0"
+                     :: "v"(x), "v"(voff), "s"(rout), "s"(r0 * row_bytes) : "memory");
+      else
+        asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 0"
+                     :: "v"(x), "v"(voff), "s"(rout), "s"(r0 * row_bytes) : "memory");
+#else
       __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff, r0 * row_bytes, NT ? 3 : 0);
+#endif
       sweep_wave_sync();                        // the stage's reads before the next rows' writes
     };
     static_assert(G % RPS == 0, "row groups");
@@ -1552,7 +1575,14 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     const int64_t pair_bytes = (int64_t)g.rows * slab * esz;
     fg.buf_ok = pair_bytes < ((int64_t)1 << 32) && (out_dtype == 0 || fg.pair_ok) && tuning().sweep_buffer;
     fg.share = tuning().sweep_share;
-    fg.store_nt = tuning().sweep_store_nt == 2 ? out_dtype != 0 : tuning().sweep_store_nt;   // auto: bf16 only
+    // auto (2): bf16 volumes always; fp32 volumes when a channel slab (L x h x w
+    // floats) is at most 6 MiB.  Measured, not derived (profiles/r05_sweep_store_shapes.txt):
+    // non-temporal fp32 stores are faster at 120x160 L=64 (the indoor c4 volume:
+    // 0.73 vs 0.69 of HBM inside the bench step), 120x161 L=64, and equal at
+    // 128x128 L=64 (slabs 4.2-4.9 MiB), slower at every slab of 7.5 MiB or more
+    // (KITTI 94x311 at L = 64 and 128, 120x160 L=128, 100x300 L=64, 96x320)
+    fg.store_nt = tuning().sweep_store_nt == 2 ? (out_dtype != 0 || slab * 4 <= ((int64_t)6 << 20))
+                                               : tuning().sweep_store_nt;
     fg.write_ref = write_ref ? 1 : 0;
     fg.store_px = store_px;
     fg.pair_bytes = fg.buf_ok ? (unsigned)pair_bytes : 0u;

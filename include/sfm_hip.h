@@ -400,7 +400,10 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     from the next lane where the offsets match (0)
  *     "sweep_store_nt"        0,1,2   k_sweep_tile's volume stores non-temporal (sc0 nt)
  *                                     so they do not evict the re-read operands
- *                                     (2: bf16 volumes only)
+ *                                     (2, default: bf16 volumes, and fp32 volumes
+ *                                     whose channel slab L*h*w*4 is <= 6 MiB --
+ *                                     measured per shape, e.g. on for the indoor
+ *                                     120x160 L=64 volume, off for KITTI 94x311)
  *     "sweep_store_px"        -1,0,1, 16-byte lane stores of k_sweep_tile (8 bf16 / 4
  *                             2,4,8   fp32 consecutive pixels through a per-wave LDS
  *                                     stage) with that many pixels per lane for the
