@@ -1010,7 +1010,14 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
         asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 0"
                      :: "v"(x), "v"(voff), "s"(rout), "s"(r0 * row_bytes) : "memory");
 #else
-      __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff, r0 * row_bytes, NT ? 3 : 0);
+      // the row offset in voffset with a literal-0 soffset, not an SGPR
+      // soffset: a 128-bit store's data VGPRs must not be overwritten by the
+      // next instruction (gfx950 stores the new value for lanes 16r+12..15
+      // otherwise, scripts/probe_store_hazard.hip), and LLVM's hazard
+      // recognizer inserts that wait state only for stores without an SGPR
+      // soffset -- the round-4 "4-byte staging miscompute" was this pair
+      // (profiles/r05_store_hazard.txt)
+      __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff + r0 * row_bytes, 0, NT ? 3 : 0);
 #endif
       sweep_wave_sync();                        // the stage's reads before the next rows' writes
     };

@@ -5,7 +5,7 @@ VGPRs stored the overwritten value for part of the wave -- with an SGPR
 soffset, the case LLVM's hazard recognizer treats as hazard-free (it inserts
 the wait state only without an SGPR soffset).  This lists every such
 instruction pair in a hipcc -S (gfx950) assembly file, per kernel.
-usage: store_hazard_check.py file.s [...]"""
+usage: store_hazard_check.py file.s|lib.so [...]"""
 import re
 import sys
 
@@ -20,13 +20,15 @@ def vregs(tok):
     return {int(m.group(1))} if m else set()
 
 
-def check(path):
+def check(path, lines=None):
+    """(kernel, store, next instruction) triples of a hipcc -S file or of
+    llvm-objdump -d output (``lines``)."""
     hits = []
     kernel = None
     prev = None
-    for raw in open(path):
-        line = raw.split(";")[0].strip()
-        m = re.match(r"^(_Z\S+):", line)
+    for raw in (lines if lines is not None else open(path)):
+        line = raw.split(";")[0].split("//")[0].strip()
+        m = re.match(r"^(?:[0-9a-f]+ )?<?(_Z[^>:\s]+)>?:", line)
         if m:
             kernel, prev = m.group(1), None
             continue
@@ -48,10 +50,38 @@ def check(path):
     return hits
 
 
+def library_device_code(so_path):
+    """llvm-objdump -d lines of every gfx950 code object bundled in a HIP
+    shared library (.hip_fatbin section, one offload bundle per translation
+    unit)."""
+    import os
+    import subprocess
+    import tempfile
+    llvm = "/opt/rocm/lib/llvm/bin"
+    out = []
+    with tempfile.TemporaryDirectory() as d:
+        fb = os.path.join(d, "fatbin")
+        subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", so_path, os.path.join(d, "x")],
+                       check=True, capture_output=True)
+        data = open(fb, "rb").read()
+        offs = [m.start() for m in re.finditer(re.escape(b"__CLANG_OFFLOAD_BUNDLE__"), data)]
+        for i, o in enumerate(offs):
+            b = os.path.join(d, f"b{i}")
+            co = os.path.join(d, f"c{i}.co")
+            open(b, "wb").write(data[o:offs[i + 1] if i + 1 < len(offs) else len(data)])
+            subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={b}", f"--output={co}"],
+                           check=True, capture_output=True)
+            dis = subprocess.run([f"{llvm}/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True,
+                                 capture_output=True, text=True).stdout
+            out.extend(dis.split("\n"))
+    return out
+
+
 if __name__ == "__main__":
     total = 0
     for p in sys.argv[1:]:
-        for k, st, nxt in check(p):
+        for k, st, nxt in check(p, library_device_code(p) if p.endswith(".so") else None):
             total += 1
             print(f"{p}: {k[:70]}\n    {st}\n    {nxt}")
     print(f"{total} store-data overwrite(s) with no wait state")

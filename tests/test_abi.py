@@ -4,6 +4,7 @@ reference's host code bit-for-bit; argument validation fails loudly."""
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -199,3 +200,19 @@ def test_score_fence_reference_counted():
     assert lib.sfm_score_fence_enable(1) == 0 and lib.sfm_score_fence_enable(1) == 0
     assert lib.sfm_score_fence_enable(0) == 0 and lib.sfm_score_fence_enable(0) == 0
     assert lib.sfm_score_fence_wait(None) == 1 and b"not enabled" in lib.sfm_last_error()
+
+
+def test_no_store_data_overwrite_hazard():
+    """Round-5 finding (the round-4 sweep miscompute): on gfx950 a 128-bit VMEM
+    store followed directly by a VALU write of one of its data VGPRs stores the
+    new value for some lanes, and LLVM only guards stores without an SGPR
+    soffset.  The product's 128-bit stores use a literal-0 soffset so the
+    compiler inserts the wait state; this checks the built library's machine
+    code for any unguarded pair (scripts/store_hazard_check.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import store_hazard_check as H
+    from sfm_amd import _lib
+    lines = H.library_device_code(_lib.LIB_PATH)
+    assert sum("buffer_store_dwordx4" in l for l in lines) > 0      # the sweep's wide stores are in there
+    hits = H.check(_lib.LIB_PATH, lines)
+    assert hits == [], hits[:3]
