@@ -122,6 +122,7 @@ const TuneKey kTuneKeys[] = {
     {"score_fp32", &sfm::Tuning::score_fp32, v_01},
     {"score_prune", &sfm::Tuning::score_prune, v_01},
     {"score_mf", &sfm::Tuning::score_mf, [](int v) { return v >= 0 && v <= 2; }},
+    {"score_mf_chunk2", &sfm::Tuning::score_mf_chunk2, [](int v) { return v >= 0 && v <= 4096; }},
     {"score_mf_prune", &sfm::Tuning::score_mf_prune, [](int v) { return v == 0 || (v >= 500 && v <= 990); }},
     {"score_mf_chunk", &sfm::Tuning::score_mf_chunk, [](int v) { return v >= 1 && v <= 4096; }},
     {"score_mf_blocks_per_cu", &sfm::Tuning::score_mf_blocks_per_cu, [](int v) { return v >= 1 && v <= 8; }},

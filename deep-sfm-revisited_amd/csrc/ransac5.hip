@@ -1568,7 +1568,8 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
                          w.cand_total, w.cntT, w.lead, w.cmap, w.skipped);
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH, w.candE,
                          w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)w.cmap, prune_pm, 1000, tuning().score_mf_chunk);
+                         kc, w.claim, (const int32_t*)w.cmap, prune_pm, 1000,
+                         tuning().score_mf_chunk2 ? tuning().score_mf_chunk2 : tuning().score_mf_chunk);
       set_last_scorer("k_score_mf2+prune");
     } else if (same && tuning().score_mf == 2) {
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,

@@ -99,6 +99,9 @@ _SIGS = [
     ("sfm_conv3_f32", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,
       ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
+    ("sfm_conv3_f32x3", ctypes.c_int,
+     [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, ctypes.c_int, _c_dp, _c_dp,
+      _c_dp, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
     ("sfm_to_channels_last_f32", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp]),
     ("sfm_score_essentials_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),

@@ -29,7 +29,17 @@ from .depth import depth_head
 from .sweep import plane_sweep_cost, quarter_intrinsics
 
 
-_ACT_DTYPE = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+_ACT_DTYPE = {"fp32": torch.float32, "fp32x3": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+
+
+def weight_exponent(w):
+    """sfm_conv3_f32x3's weight scale: the power of two 2^e with 2^e max|w| in
+    [2^13, 2^14) (the lo terms of the split stay in the f16 normal range, the
+    hi terms far from its maximum), clamped to the ABI's [-24, 24]."""
+    m = float(w.abs().max())
+    if not (m > 0.0 and math.isfinite(m)):
+        return 0
+    return max(-24, min(24, 13 - math.frexp(m)[1] + 1))
 
 
 def convbn_3d(in_planes, out_planes, kernel_size=3, stride=1, pad=1):
@@ -163,14 +173,18 @@ class CostRegularization(nn.Module):
                 bi[:cout] = bias.cpu()
                 packed.append(dict(w=wp.to(device=device, dtype=wdt).contiguous(),
                                    scale=sc.to(device), bias=bi.to(device), cin=cin, cout=cout, relu=relu,
-                                   resid=resid))
+                                   resid=resid, wexp=weight_exponent(wp)))
         self._packed, self._packed_key = packed, key
         return packed
 
     def forward(self, cost, precision="fp32"):
         """cost [B, Cin, L, h, w] fp32 or bf16 (the sweep's volume) -> [B, 1, L, h, w] fp32.
         ``precision``: "fp32" (default: fp32 activations, weights and
-        accumulation, sfm_conv3_f32, the reference's precision), "fp16" (fp16
+        accumulation, sfm_conv3_f32, the reference's precision), "fp32x3"
+        (the same fp32 activations and weights, each product formed from a
+        two-term f16 split of both operands on the f16 matrix cores,
+        sfm_conv3_f32x3: ~2^-21 per product, within the float64 depth bars),
+        "fp16" (fp16
         activations and weights, fp32 accumulation: sfm_conv3_f16, the
         reference's precision under cfg.MIXED_PREC) or "bf16" (bf16, fp32
         accumulation: sfm_conv3_bf16, the fastest opt-in)."""
@@ -188,9 +202,15 @@ class CostRegularization(nn.Module):
         lib = _lib.load()
         dev = cost.device
         adt = _ACT_DTYPE[precision]
-        suffix = {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}[precision]
+        suffix = {"fp32": "f32", "fp32x3": "f32", "fp16": "f16", "bf16": "bf16"}[precision]
         to_cl = getattr(lib, "sfm_to_channels_last_" + suffix)
-        conv = getattr(lib, "sfm_conv3_" + suffix)
+        if precision == "fp32x3":
+            # the split-f16 kernel takes the weights' power-of-two exponent after them
+            x3 = lib.sfm_conv3_f32x3
+            fn_name = "sfm_conv3_f32x3"
+        else:
+            conv = getattr(lib, "sfm_conv3_" + suffix)
+            fn_name = "sfm_conv3_" + suffix
         with torch.cuda.device(dev):
             stream = _lib.stream_ptr(dev)
             x = torch.empty((B, L, h, w, C), dtype=adt, device=dev)
@@ -205,10 +225,15 @@ class CostRegularization(nn.Module):
                 else:
                     dst = next(bb for bb in bufs if bb is not cur and bb is not keep)
                 res = keep if lay["resid"] else None
-                rc = conv(_lib.ptr(cur), B, lay["cin"], L, h, w, _lib.ptr(lay["w"]), _lib.ptr(lay["scale"]),
-                          _lib.ptr(lay["bias"]), None if res is None else _lib.ptr(res), 1 if lay["relu"] else 0,
-                          lay["cout"], _lib.ptr(dst), stream)
-                _lib.check(rc, "sfm_conv3_" + suffix)
+                if precision == "fp32x3":
+                    rc = x3(_lib.ptr(cur), B, lay["cin"], L, h, w, _lib.ptr(lay["w"]), lay["wexp"],
+                            _lib.ptr(lay["scale"]), _lib.ptr(lay["bias"]), None if res is None else _lib.ptr(res),
+                            1 if lay["relu"] else 0, lay["cout"], _lib.ptr(dst), stream)
+                else:
+                    rc = conv(_lib.ptr(cur), B, lay["cin"], L, h, w, _lib.ptr(lay["w"]), _lib.ptr(lay["scale"]),
+                              _lib.ptr(lay["bias"]), None if res is None else _lib.ptr(res), 1 if lay["relu"] else 0,
+                              lay["cout"], _lib.ptr(dst), stream)
+                _lib.check(rc, fn_name)
                 # cost0 after dres0 (layer 1) and after every residual add is the next block's input
                 if li == 1 or lay["resid"]:
                     keep = dst

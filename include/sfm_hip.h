@@ -378,6 +378,19 @@ int sfm_conv3_f32(const float* in, int batch, int cin, int depth, int h, int w, 
                   const float* scale, const float* bias, const float* residual, int relu, int cout, float* out,
                   void* stream);
 
+/* sfm_conv3_f32's layer with fp32 products formed on the f16 matrix cores
+ * (conv_precision "fp32x3", round 5): both operands split in two f16 terms
+ * (x = x_hi + x_lo; the weights first scaled by 2^wexp so their lo terms stay
+ * normal, the scale folded back in the epilogue) and
+ * w x ~ w_hi x_hi + w_hi x_lo + w_lo x_hi, three v_mfma_f32_32x32x16_f16 per
+ * k = 16 into fp32 accumulators (~2^-21 relative per product).  Same layouts
+ * and arguments as sfm_conv3_f32, plus wexp in [-24, 24] (the caller picks it
+ * so that 2^wexp max|w| < 2^15).  Replaces the same Conv3d layers
+ * (models/PSNet.py:79-102, applied at 159-165). */
+int sfm_conv3_f32x3(const float* in, int batch, int cin, int depth, int h, int w, const float* weights, int wexp,
+                    const float* scale, const float* bias, const float* residual, int relu, int cout, float* out,
+                    void* stream);
+
 /* [batch][channels][plane] float32 (in_dtype 0) or bfloat16 (1) ->
  * [batch][plane][channels] float32 (channels a multiple of 4): the sweep's
  * cost volume into sfm_conv3_f32's layout. */
@@ -425,6 +438,8 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     2 by default; exact by proof, same counts)
  *     "score_mf_chunk"        1..4096 k_score_mf2's smallest claimed unit range, in
  *                                     (span, 32-candidate tile) units (64)
+ *     "score_mf_chunk2"       0..4096 the same for the pruned second launch (0: as
+ *                                     score_mf_chunk)
  *     "score_mf_prune"        0, 500..990  count-bound pruning in k_score_mf2 (880):
  *                                     every candidate scored on the first N per
  *                                     mille of each pair's 1024-point spans, then

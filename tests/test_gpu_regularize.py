@@ -314,6 +314,104 @@ def test_conv_layer_f32(cuda, B, cin, D, h, w, relu, resid, cout):
     assert float(err.max()) <= 0, float((got - want).abs().max())
 
 
+# fp32x3 path (precision="fp32x3": sfm_conv3_f32x3, each fp32 product from a
+# two-term f16 split of both operands on the f16 matrix cores).  One layer:
+# every product within ~3 x 2^-22 relative (the two splits and the dropped
+# lo x lo term; an activation's lo term can be subnormal: 2^-24 absolute),
+# then the f32 accumulation as sfm_conv3_f32 -- the f32 layer bound holds.
+
+def _conv_f32x3(cuda, x, wt, scale, bias, res, relu, cout):
+    from sfm_amd import _lib
+    from sfm_amd.regularize import weight_exponent
+    cin = x.shape[1]
+    wp = torch.zeros(27, 32, cin)
+    wp[:, :cout] = wt.permute(2, 3, 4, 0, 1).reshape(27, cout, cin)
+    sc, bi = torch.ones(32), torch.zeros(32)
+    sc[:cout], bi[:cout] = scale, bias
+    xcl = x.permute(0, 2, 3, 4, 1).contiguous().to(cuda)
+    rcl = None if res is None else res.permute(0, 2, 3, 4, 1).contiguous().to(cuda)
+    B, _, D, h, w = x.shape
+    out = torch.empty((B, D, h, w, 32) if cout == 32 else (B, D, h, w), dtype=torch.float32, device=cuda)
+    e = weight_exponent(wp)
+    wp, sc, bi = wp.to(cuda), sc.to(cuda), bi.to(cuda)
+    with torch.cuda.device(cuda):
+        _lib.check(_lib.load().sfm_conv3_f32x3(_lib.ptr(xcl), B, cin, D, h, w, _lib.ptr(wp), e, _lib.ptr(sc),
+                                               _lib.ptr(bi), None if rcl is None else _lib.ptr(rcl), 1 if relu else 0,
+                                               cout, _lib.ptr(out), _lib.stream_ptr(cuda)), "sfm_conv3_f32x3")
+    out = out.cpu()
+    return out.permute(0, 4, 1, 2, 3) if cout == 32 else out
+
+
+@pytest.mark.parametrize("B,cin,D,h,w,relu,resid,cout", [
+    (1, 32, 3, 4, 64, False, False, 32),
+    (2, 64, 5, 7, 70, True, False, 32),
+    (1, 32, 4, 9, 131, False, True, 32),
+    (1, 32, 6, 5, 33, False, False, 1),
+    (1, 64, 1, 1, 1, True, False, 32),
+    (1, 64, 3, 17, 65, True, True, 32),
+])
+def test_conv_layer_f32x3(cuda, B, cin, D, h, w, relu, resid, cout):
+    g = torch.Generator().manual_seed(B * 100 + cin + D + h + w + 9)
+    x = torch.randn(B, cin, D, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1
+    scale = 0.5 + torch.rand(cout, generator=g)
+    bias = 0.3 * torch.randn(cout, generator=g)
+    res = torch.randn(B, 32, D, h, w, generator=g) if resid else None
+    xd, wd = x.double(), wt.double()
+    want = F.conv3d(xd, wd, None, 1, 1) * scale.double().view(1, -1, 1, 1, 1) + bias.double().view(1, -1, 1, 1, 1)
+    mag = F.conv3d(xd.abs(), wd.abs(), None, 1, 1) * scale.double().view(1, -1, 1, 1, 1)
+    if relu:
+        want = torch.relu(want)
+    if res is not None:
+        want = want + res.double()
+    got = _conv_f32x3(cuda, x, wt, scale, bias, res, relu, cout).double()
+    if cout == 1:
+        want, mag = want[:, 0], mag[:, 0]
+    err = (got - want).abs() - (2e-5 * mag + 1e-6)
+    assert float(err.max()) <= 0, float((got - want).abs().max())
+    # and as close to the float64 conv as the f32-MFMA layer is, within 4x
+    ref32 = _conv_f32(cuda, x, wt, scale, bias, res, relu, cout).double()
+    e3 = float((got - want).norm() / want.norm())
+    e32 = float((ref32 - want).norm() / want.norm())
+    assert e3 <= 4 * e32 + 1e-7, (e3, e32)
+
+
+@pytest.mark.parametrize("B,cin,L,h,w", [(1, 64, 16, 12, 20), (1, 32, 7, 5, 67)])
+def test_stack_f32x3_vs_oracle(cuda, B, cin, L, h, w):
+    """12 fp32x3 layers vs the fp32 oracle stack: relative L2 <= 2e-5 (the
+    fp32 path's 1e-5 plus the split's ~2^-21 per product)."""
+    m = _module(11 + L, cin)
+    cost = torch.randn(B, cin, L, h, w, generator=torch.Generator().manual_seed(L))
+    got = m.to(cuda)(cost.to(cuda), precision="fp32x3").cpu()
+    m = m.cpu()
+    want = R.regularize_fp32(m, cost)
+    r = float((got - want).norm() / want.norm())
+    assert got.shape == want.shape and r <= 2e-5, r
+
+
+def test_psnet_fp32x3_depth_vs_float64_reference(cuda, golden):
+    """psnet_depth with the split-f16 fp32 regularisation (sweep ->
+    sfm_conv3_f32x3 x 12 -> head) vs the float64 reference depth: the fp32
+    path's bars -- median <= 1e-5 and max <= 1e-4 relative, and within 20x of
+    the reference's own float32 error at both statistics."""
+    from sfm_amd.regularize import psnet_depth
+    g, m = _psnet64(golden)
+    inp = g["input"]
+    L, md = int(inp["nlabel"]), float(inp["min_depth"])
+    hw = tuple(int(x) for x in inp["image_hw"])
+    d = lambda k: torch.from_numpy(k).to(cuda)
+    got = psnet_depth(d(inp["ref_fea"]), d(inp["tgt_fea"]), d(inp["pose_rescaled"])[:, 0], d(inp["K"]),
+                      d(inp["Kinv"]), m.to(cuda), L, md, out_hw=hw, precision="fp32x3").cpu()
+    want = torch.from_numpy(g["out64"]["depth"])
+    ref32 = _rel(torch.from_numpy(g["out32"]["depth"]), want)
+    r = _rel(got, want)
+    msg = dict(ours_median=float(r.median()), ours_max=float(r.max()), ref32_median=float(ref32.median()),
+               ref32_max=float(ref32.max()))
+    print(msg)
+    assert float(r.median()) <= 1e-5 and float(r.max()) <= 1e-4, msg
+    assert float(r.median()) <= 20 * float(ref32.median()) and float(r.max()) <= 20 * float(ref32.max()), msg
+
+
 @pytest.mark.parametrize("shape", [(2, 64, 5, 7, 13), (1, 32, 4, 6, 9)])
 def test_channels_last_f32_exact(cuda, shape):
     from sfm_amd import _lib
