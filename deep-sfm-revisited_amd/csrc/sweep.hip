@@ -1009,6 +1009,9 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       else
         asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 0"
                      :: "v"(x), "v"(voff), "s"(rout), "s"(r0 * row_bytes) : "memory");
+#elif defined(SFM_SWEEP_SGPR_SOFFSET)
+      // experiment builds only: the round-4 form (row offset as the SGPR soffset)
+      __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff, r0 * row_bytes, NT ? 3 : 0);
 #else
       // the row offset in voffset with a literal-0 soffset, not an SGPR
       // soffset: a 128-bit store's data VGPRs must not be overwritten by the
