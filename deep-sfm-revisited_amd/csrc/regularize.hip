@@ -754,8 +754,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void k_conv3_f32(
 // and 2^wexp w is below the f16 maximum (65504).
 // A stage is (dz, 16-channel quarter), as in k_conv3_f32; a staged pixel (or
 // weight row) is 64 B: chunks 0-1 the hi halves of channels 0-7 / 8-15,
-// chunks 2-3 the lo halves, XOR-swizzled by (p >> 2) & 3.  The split happens
-// in the staging loop (one float4 -> 8 B hi + 8 B lo).
+// chunks 2-3 the lo halves, XOR-swizzled by (p >> 2) & 3.  The next stage's
+// fp32 operands load into registers under the current stage's MFMAs (as in
+// k_conv3) and are split on their way into LDS (one float4 -> 8 B hi + 8 B lo).
 // ---------------------------------------------------------------------------
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
@@ -788,69 +789,103 @@ __global__ __launch_bounds__(kConvThreads, 2) void k_conv3_x3(
   const int nq = cin / kF32Ch;
   const int64_t plane = (int64_t)H * W;
   const float wmul = __builtin_ldexpf(1.0f, wexp);
+  // the stages: (dz, quarter q) over the planes inside the volume (zero
+  // padding contributes nothing), staged through registers one ahead
+  const int dz0 = d == 0 ? 1 : 0, dz1 = d == D - 1 ? 2 : 3;
+  const int nstage = (dz1 - dz0) * nq;
+
+  // staging map (hoisted, as k_conv3's): thread t loads float4 t&3 of halo
+  // column t>>2 (0..63) in all 10 rows, threads < 80 one float4 of columns
+  // 64/65, and weight float4 t&3 of cout (t>>2)&31 for taps t>>7 + 2k
+  const int mc = tid & 3, mpx = tid >> 2;
+  const int mgx = x0 - 1 + mpx;
+  const bool mvx = mgx >= 0 && mgx < W;
+  const bool hasx = tid < kHaloY * 8;
+  const int epx = 64 + ((tid >> 2) & 1), ery = tid >> 3;
+  const int egx = x0 - 1 + epx, egy = y0 - 1 + ery;
+  const bool evalid = hasx && egx < W && egy >= 0 && egy < H;
+  const int wco = (tid >> 2) & 31, wt0 = tid >> 7;
+  float4 pin[kHaloY + 1], pw[5];
+  auto fetch = [&](int s) {
+    const int dz = dz0 + s / nq, q = s - (s / nq) * nq;
+    const float* pl = in + ((int64_t)b * D + (d + dz - 1)) * plane * cin + q * kF32Ch + mc * 4;
+#pragma unroll
+    for (int ry = 0; ry < kHaloY; ++ry) {
+      const int gy = y0 - 1 + ry;
+      float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (gy >= 0 && gy < H && mvx) v = *reinterpret_cast<const float4*>(pl + ((int64_t)gy * W + mgx) * cin);
+      pin[ry] = v;
+    }
+    {
+      float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (evalid) v = *reinterpret_cast<const float4*>(pl + ((int64_t)egy * W + egx) * cin);
+      pin[kHaloY] = v;
+    }
+    const float* wb = wpk + (int64_t)dz * 9 * 32 * cin + q * kF32Ch + mc * 4;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      if (wt0 + 2 * k < 9) v = *reinterpret_cast<const float4*>(wb + ((wt0 + 2 * k) * 32 + wco) * cin);
+      pw[k] = v;
+    }
+  };
+  // one float4 (4 channels, mc) -> 8 B of hi halves in chunk mc >> 1 and 8 B
+  // of lo halves in chunk 2 + (mc >> 1) of a 64-byte LDS row
+  auto put = [&](unsigned char* row, int sw, float4 v) {
+    uint2 hi, lo;
+    split_f16x4(v, hi, lo);
+    *reinterpret_cast<uint2*>(row + (mc & 1) * 8 + swz4(mc >> 1, sw) * 16) = hi;
+    *reinterpret_cast<uint2*>(row + (mc & 1) * 8 + swz4(2 + (mc >> 1), sw) * 16) = lo;
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int ry = 0; ry < kHaloY; ++ry) put(lds_in + (ry * kHaloX + mpx) * kF32Pix, mpx, pin[ry]);
+    if (hasx) put(lds_in + (ery * kHaloX + epx) * kF32Pix, epx, pin[kHaloY]);
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (wt0 + 2 * k < 9) {
+        float4 v = pw[k];
+        v.x *= wmul; v.y *= wmul; v.z *= wmul; v.w *= wmul;
+        put(lds_w + ((wt0 + 2 * k) * 32 + wco) * kF32Pix, wco, v);
+      }
+  };
 
   f32x16 acc[4];
 #pragma unroll
   for (int o = 0; o < 4; ++o)
     for (int i = 0; i < 16; ++i) acc[o][i] = 0.0f;
 
-  for (int dz = 0; dz < 3; ++dz) {
-    const int zd = d + dz - 1;
-    if (zd < 0 || zd >= D) continue;                         // zero padding: no contribution (block-uniform)
-    const float* pl = in + ((int64_t)b * D + zd) * plane * cin;
-    for (int q = 0; q < nq; ++q) {
-      __syncthreads();                                       // the previous stage's operand reads are done
-      // input halo: 10 rows x 66 pixels x 4 float4 of the quarter -> hi / lo halves
-      for (int i = tid; i < kHaloY * kHaloX * 4; i += kConvThreads) {
-        const int c = i & 3, px = (i >> 2) % kHaloX, ry = (i >> 2) / kHaloX;
-        const int gx = x0 - 1 + px, gy = y0 - 1 + ry;
-        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (gx >= 0 && gx < W && gy >= 0 && gy < H)
-          v = *reinterpret_cast<const float4*>(pl + ((int64_t)gy * W + gx) * cin + q * kF32Ch + c * 4);
-        uint2 hi, lo;
-        split_f16x4(v, hi, lo);
-        unsigned char* base = lds_in + (ry * kHaloX + px) * kF32Pix + (c & 1) * 8;
-        *reinterpret_cast<uint2*>(base + swz4(c >> 1, px) * 16) = hi;
-        *reinterpret_cast<uint2*>(base + swz4(2 + (c >> 1), px) * 16) = lo;
-      }
-      // weights: 9 (dy, dx) taps x 32 cout x 4 float4, scaled by 2^wexp, -> hi / lo
-      for (int i = tid; i < 9 * 32 * 4; i += kConvThreads) {
-        const int c = i & 3, co = (i >> 2) & 31, t = i >> 7;
-        float4 v = *reinterpret_cast<const float4*>(wpk + ((int64_t)(dz * 9 + t) * 32 + co) * cin + q * kF32Ch + c * 4);
-        v.x *= wmul; v.y *= wmul; v.z *= wmul; v.w *= wmul;
-        uint2 hi, lo;
-        split_f16x4(v, hi, lo);
-        unsigned char* base = lds_w + (t * 32 + co) * kF32Pix + (c & 1) * 8;
-        *reinterpret_cast<uint2*>(base + swz4(c >> 1, co) * 16) = hi;
-        *reinterpret_cast<uint2*>(base + swz4(2 + (c >> 1), co) * 16) = lo;
-      }
-      __syncthreads();
+  fetch(0);
+  for (int s = 0; s < nstage; ++s) {
+    __syncthreads();                                         // the previous stage's operand reads are done
+    commit();
+    __syncthreads();
+    if (s + 1 < nstage) fetch(s + 1);                        // global loads in flight under the MFMAs
 #pragma unroll 1
-      for (int dx = 0; dx < 3; ++dx) {
-        const int p = wcol + r + dx;
-        f16x8 wh[3], wl[3], xh[6], xl[6];
+    for (int dx = 0; dx < 3; ++dx) {
+      const int p = wcol + r + dx;
+      f16x8 wh[3], wl[3], xh[6], xl[6];
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-          const unsigned char* wrowp = lds_w + ((dy * 3 + dx) * 32 + r) * kF32Pix;
-          wh[dy] = *reinterpret_cast<const f16x8*>(wrowp + swz4(kh, r) * 16);
-          wl[dy] = *reinterpret_cast<const f16x8*>(wrowp + swz4(2 + kh, r) * 16);
-        }
-#pragma unroll
-        for (int ir = 0; ir < 6; ++ir) {
-          const unsigned char* px = lds_in + ((wrow + ir) * kHaloX + p) * kF32Pix;
-          xh[ir] = *reinterpret_cast<const f16x8*>(px + swz4(kh, p) * 16);
-          xl[ir] = *reinterpret_cast<const f16x8*>(px + swz4(2 + kh, p) * 16);
-        }
-        // hi x hi first into each accumulator, then the two cross terms
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-          for (int o = 0; o < 4; ++o) {
-            acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[dy], xh[o + dy], acc[o], 0, 0, 0);
-            acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[dy], xl[o + dy], acc[o], 0, 0, 0);
-            acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[dy], xh[o + dy], acc[o], 0, 0, 0);
-          }
+      for (int dy = 0; dy < 3; ++dy) {
+        const unsigned char* wrowp = lds_w + ((dy * 3 + dx) * 32 + r) * kF32Pix;
+        wh[dy] = *reinterpret_cast<const f16x8*>(wrowp + swz4(kh, r) * 16);
+        wl[dy] = *reinterpret_cast<const f16x8*>(wrowp + swz4(2 + kh, r) * 16);
       }
+#pragma unroll
+      for (int ir = 0; ir < 6; ++ir) {
+        const unsigned char* px = lds_in + ((wrow + ir) * kHaloX + p) * kF32Pix;
+        xh[ir] = *reinterpret_cast<const f16x8*>(px + swz4(kh, p) * 16);
+        xl[ir] = *reinterpret_cast<const f16x8*>(px + swz4(2 + kh, p) * 16);
+      }
+      // hi x hi first into each accumulator, then the two cross terms
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[dy], xh[o + dy], acc[o], 0, 0, 0);
+          acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[dy], xl[o + dy], acc[o], 0, 0, 0);
+          acc[o] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[dy], xh[o + dy], acc[o], 0, 0, 0);
+        }
     }
   }
 
