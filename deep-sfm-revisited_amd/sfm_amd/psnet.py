@@ -112,7 +112,10 @@ class PSNet(CostRegularization):
     (CostRegularization): "auto" (default) follows the reference --
     PSNet.py:159-165 in float32, or in float16 under cfg.MIXED_PREC, the
     autocast SFMnet.py:164 wraps the depth estimator in (cfgs/kitti.yml:10) --
-    so it resolves to "fp32" or "fp16"; "bf16" is the fastest opt-in path;
+    so it resolves to "fp32x3" (fp32 operands, each product from a two-term
+    f16 split on the f16 matrix cores: within the float64 fixture's depth bars
+    at 3x the speed of "fp32", the f32-MFMA path, which stays selectable) or
+    "fp16"; "bf16" is the fastest opt-in path;
     ``cost_dtype`` the sweep volume's storage."""
 
     def __init__(self, nlabel, mindepth=None, cfg=None, feature_fn=None, cost_dtype=torch.float32,
@@ -126,8 +129,8 @@ class PSNet(CostRegularization):
         self.mindepth = float(c.MIN_DEPTH)            # the reference reads cfg.MIN_DEPTH too (PSNet.py:44)
         self.cost_dtype = cost_dtype
         if conv_precision == "auto":
-            conv_precision = "fp16" if c.get("MIXED_PREC", False) else "fp32"
-        if conv_precision not in ("fp32", "fp16", "bf16"):
+            conv_precision = "fp16" if c.get("MIXED_PREC", False) else "fp32x3"
+        if conv_precision not in ("fp32", "fp32x3", "fp16", "bf16"):
             raise ValueError(f"unknown conv precision {conv_precision!r}")
         self.conv_precision = conv_precision
         self.feature_extraction = FeatureExtraction() if feature_fn is None else feature_fn

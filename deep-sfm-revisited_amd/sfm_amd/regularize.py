@@ -9,8 +9,10 @@ its application at PSNet.py:159-165:
     cost0 = classify(cost0)                      # [B, 1, L, h, w]
 
 ``CostRegularization.forward`` runs the 12 Conv3d layers as
-``sfm_conv3_f32`` launches (default ``precision="fp32"``: fp32 activations
-and weights on the f32 matrix cores, the reference's precision), with
+``sfm_conv3_f32x3`` launches (default ``precision="fp32x3"``: the
+reference's fp32 activations and weights, each product formed from split-f16
+operands on the f16 matrix cores; ``precision="fp32"`` is the same on the
+f32 matrix cores, ``sfm_conv3_f32``), with
 ``precision="fp16"`` as ``sfm_conv3_f16`` launches (float16 channels-last
 activations and weights, fp32 accumulation: the precision of the reference's
 Conv3d layers under ``cfg.MIXED_PREC`` autocast, SFMnet.py:164) or, with
@@ -177,13 +179,14 @@ class CostRegularization(nn.Module):
         self._packed, self._packed_key = packed, key
         return packed
 
-    def forward(self, cost, precision="fp32"):
+    def forward(self, cost, precision="fp32x3"):
         """cost [B, Cin, L, h, w] fp32 or bf16 (the sweep's volume) -> [B, 1, L, h, w] fp32.
-        ``precision``: "fp32" (default: fp32 activations, weights and
-        accumulation, sfm_conv3_f32, the reference's precision), "fp32x3"
-        (the same fp32 activations and weights, each product formed from a
-        two-term f16 split of both operands on the f16 matrix cores,
-        sfm_conv3_f32x3: ~2^-21 per product, within the float64 depth bars),
+        ``precision``: "fp32x3" (default: the reference's fp32 activations
+        and weights, each product formed from a two-term f16 split of both
+        operands on the f16 matrix cores, sfm_conv3_f32x3: ~2^-21 per product,
+        within the float64 depth bars at 3x the speed of "fp32"), "fp32"
+        (fp32 operands on the f32 matrix cores, sfm_conv3_f32: float32
+        arithmetic exactly, in another summation order),
         "fp16" (fp16
         activations and weights, fp32 accumulation: sfm_conv3_f16, the
         reference's precision under cfg.MIXED_PREC) or "bf16" (bf16, fp32

@@ -554,7 +554,7 @@ def test_default_psnet_module_vs_float64_reference(cuda, golden):
         calls.append(img.shape)
         return feas[(len(calls) - 1) % 2]
     net = PSNet(L, md, cfg=c, feature_fn=feature_fn).to(cuda).eval()
-    assert net.conv_precision == "fp32"
+    assert net.conv_precision == "fp32x3"
     net.load_state_dict({k: torch.from_numpy(v) for k, v in g["state"].items()}, strict=False)
     img = torch.zeros(1, 3, H, W, device=cuda)
     d = lambda k: torch.from_numpy(k).to(cuda)
