@@ -67,4 +67,4 @@ def main(R):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r04")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r05")

@@ -33,7 +33,7 @@ def short_name(name):
 
 
 def kernel_key(name):
-    if "k_score_mf" in name or "k_mf_cands" in name:   # mangled names in the rocprof CSV
+    if "k_score_mf" in name or "k_mf_cands" in name or "k_mf2_" in name:   # mangled names in the rocprof CSV
         return "ransac_score"
     if "k_sweep_tile" in name:
         return "plane_sweep"
@@ -52,9 +52,8 @@ WORKLOADS = {"c2": (8, 8, 128, "fp32"), "c3": (4, 8, 128, "bf16"), "c4": (8, 4, 
 def main(src, dst, config="c2"):
     # per (path key, kernel): one list of per-dispatch values per counter.  A
     # path key can hold several kernels of one step (ransac_score = k_mf_cands
-    # + k_score_mf2, one launch each): its per-step figure is the SUM of the
-    # kernels' per-dispatch means (round 2's summaries averaged the
-    # dispatches of both kernels together, which halved the scoring traffic)
+    # + 2 x k_score_mf2 + k_mf2_lead + k_mf2_keep with pruning): its per-step
+    # figure is the SUM of all their dispatches per step
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True)):
         acc = collections.defaultdict(float)
@@ -70,9 +69,13 @@ def main(src, dst, config="c2"):
     out = {}
     for k, names in keys.items():
         m = collections.defaultdict(float)
+        # per step: every dispatch of the key's kernels summed over the steps,
+        # the step count being the fewest dispatches of any of them (k_mf_cands
+        # once per step; the pruned scorer launches k_score_mf2 twice)
+        steps = min(max(len(v) for v in per[(k, name)].values()) for name in names)
         for name in names:
             for c, v in per[(k, name)].items():
-                m[c] += sum(v) / len(v)                       # mean over this kernel's dispatches
+                m[c] += sum(v) / steps
         d = {"launches_sampled": {short_name(n): max(len(v) for v in per[(k, n)].values()) for n in names}}
         d.update({c: round(v, 1) for c, v in sorted(m.items())})
         if "FETCH_SIZE" in m:
