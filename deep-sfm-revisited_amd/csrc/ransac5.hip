@@ -74,6 +74,7 @@ struct Workspace {
   unsigned long long* claim;    // [9] k_score_mf2's range-claim counters and finished-block count (zero between launches)
   int32_t* cmap;       // [B][Cmax] k_mf2_keep: the kept candidates of each pair
   int32_t* lead;       // [4][64] k_mf2_lead / _keep: leader count, index, rest count, kept candidates
+  int32_t* bnd;        // [4][64] k_mf2_split: span boundaries of the pruned launches per pair
   double* pack;        // [n_max][4] (last: its size is the only n_max-dependent one)
 };
 
@@ -107,6 +108,7 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   t.claim = (unsigned long long*)take(kMf2ClaimBytes);
   t.cmap = (int32_t*)take(bc * C * 4);
   t.lead = (int32_t*)take(SFM_MAX_BATCH * 4 * 4);
+  t.bnd = (int32_t*)take(SFM_MAX_BATCH * 4 * 4);
   t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
   if (w) *w = t;
   return off;
@@ -1537,8 +1539,9 @@ struct ScoreBufs {
   int32_t* cntR;
   unsigned long long* claim;   // [9] k_score_mf2's range-claim counters and finished-block count
   int32_t* cmap = nullptr;     // count-bound pruning (k_mf2_lead / _keep): kept candidates, the
-  int32_t* lead = nullptr;     // leader records (their [3] = kept candidates), the evaluations skipped
+  int32_t* lead = nullptr;     // leader records (their [3] = kept candidates), the evaluations skipped,
   unsigned long long* skipped = nullptr;
+  int32_t* bnd = nullptr;      // the launches' span boundaries per pair (k_mf2_split)
 };
 
 // score_precision with the low-precision form folded in: 64, 32 / 16 (held in
@@ -1558,22 +1561,29 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
     const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
     const dim3 g2(std::max(1, cus)), b2(kMf2Waves * 64);
     if (same && tuning().score_mf == 2 && prune_pm > 0) {
-      // count-bound pruning: every candidate on the first prune_pm per mille
-      // of each pair's spans, k_mf2_lead + k_mf2_keep, the kept ones on the rest
+      // count-bound pruning: A every candidate on the first prune_pm per mille
+      // of each pair's spans; k_mf2_split picks the pair's pruning point sB
+      // from its inlier ratio; B every candidate up to sB; k_mf2_lead +
+      // k_mf2_keep; C the kept candidates on the rest
+      const int ch = tuning().score_mf_chunk;
+      const int ch2 = tuning().score_mf_chunk2 ? tuning().score_mf_chunk2 : ch;
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, tuning().score_mf_chunk);
-      hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax, prune_pm,
-                         w.cand_total, w.candE, w.cntT, kc, w.lead);
-      hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax, prune_pm,
-                         w.cand_total, w.cntT, w.lead, w.cmap, w.skipped);
+                         kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr, 0, ch);
+      hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, prune_pm, tuning().score_mf_prune_margin,
+                         w.cand_total, w.cntT, w.bnd);
+      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
+                         kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
+      hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
+                         (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead);
+      hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax,
+                         (const int32_t*)w.bnd, w.cand_total, w.cntT, w.lead, w.cmap, w.skipped);
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH, w.candE,
-                         w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)w.cmap, prune_pm, 1000,
-                         tuning().score_mf_chunk2 ? tuning().score_mf_chunk2 : tuning().score_mf_chunk);
+                         w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap, 0, 0, (const int32_t*)w.bnd, 2, ch2);
       set_last_scorer("k_score_mf2+prune");
     } else if (same && tuning().score_mf == 2) {
       hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)nullptr, 0, 1000, tuning().score_mf_chunk);
+                         kc, w.claim, (const int32_t*)nullptr, 0, 1000, (const int32_t*)nullptr, 0,
+                         tuning().score_mf_chunk);
       set_last_scorer("k_score_mf2");
     } else if (same) {
       hipLaunchKernelGGL((k_score_mf<Src, true>), gmf, dim3(kMfWaves * 64), 0, s, src, pp, bc, cmax,
@@ -1839,6 +1849,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     ScoreBufs sb{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim};
     sb.cmap = w.cmap;
     sb.lead = w.lead;
+    sb.bnd = w.bnd;
     sb.skipped = w.skipped;
     score_dispatch(src, pp, bc, cmax, sb, kc, mp, use_mf, same, prec, fast, fast32, cus, grid, s, mf2_pm);
   }

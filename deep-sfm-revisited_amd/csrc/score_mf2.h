@@ -26,9 +26,10 @@
 //     pair or ends.
 //
 // Count-bound pruning (round 5, tuning key score_mf_prune): the launch can
-// cover only a range of each pair's spans (sp_lo .. sp_hi, in per-mille of
-// the span count), and the candidates can be a compacted subset whose counts
-// go to cntT[cmap[j]] (k_mf2_lead / k_mf2_keep below).
+// cover only a range of each pair's spans (sp_lo .. sp_hi, in per mille of
+// the span count, or per-pair boundaries in device memory), and the
+// candidates can be a compacted subset whose counts go to cntT[cmap[j]]
+// (k_mf2_split / k_mf2_lead / k_mf2_keep below).
 //
 // Registers (gfx950, 3 waves per SIMD = 168 VGPRs): 2 x 48 accumulators + 16
 // A + 12 B + 32 decision strings in the loop.  The round 2-4 schedule and
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
     const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
     ScoreConsts kc, unsigned long long* __restrict__ claim, const int32_t* __restrict__ cmap, int sp_lo,
-    int sp_hi, int min_chunk) {
+    int sp_hi, const int32_t* __restrict__ bnd, int phase, int min_chunk) {
   // one count array: this kernel runs only when num_test == num_ransac_test,
   // so the preselection count is the score and k_select reads cntT for both
   __shared__ __attribute__((aligned(16))) _Float16 s_frag[kMf2Tiles][3][64][8];
@@ -178,7 +179,10 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       const int ct = cand_total[b];
       const int tiles = (ct + kKC - 1) / kKC;
       const int all = mf2_spans(max(pp.test[b], pp.rtest[b]));
-      const int s0 = mf2_span_at(all, sp_lo), s1 = mf2_span_at(all, sp_hi);
+      // the launch's spans: per mille of the pair's spans, or (bnd) the span
+      // boundaries phase and phase + 1 that k_mf2_split chose for the pair
+      const int s0 = bnd ? bnd[phase * SFM_MAX_BATCH + b] : mf2_span_at(all, sp_lo);
+      const int s1 = bnd ? bnd[(phase + 1) * SFM_MAX_BATCH + b] : mf2_span_at(all, sp_hi);
       s_first[b] = acc;
       s_tiles[b] = tiles;
       s_ctot[b] = ct;
@@ -428,10 +432,10 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   }
 }
 
-// Count-bound pruning between two k_score_mf2 launches (tuning key
-// score_mf_prune = pm; only for SFMnet's num_test == num_ransac_test without
-// per-hypothesis scores).  The first launch scores every candidate of pair b
-// on its first n1 points (spans [0, spans * pm / 1000)); then
+// Count-bound pruning (tuning key score_mf_prune = pm; only for SFMnet's
+// num_test == num_ransac_test without per-hypothesis scores).  Launches A
+// and B score every candidate of pair b on its first n1 points (spans [0,
+// sB), k_mf2_split above); then
 //   k_mf2_lead  (kLeadBlocks blocks per pair) takes the leader, the first
 //               candidate with the largest partial count, and counts its
 //               inliers on the remaining points [n1, M) with the exact
@@ -456,13 +460,57 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 // phase), 3: kept candidates (the second launch's cand_total).
 constexpr int kLeadBlocks = 32;
 
-__device__ __forceinline__ int mf2_n1(const PairParams& pp, int b, int pm) {
+// the points the launches before the pruning scored: spans [0, bnd[2][b])
+__device__ __forceinline__ int mf2_n1(const PairParams& pp, int b, const int32_t* bnd) {
   const int M = max(pp.test[b], pp.rtest[b]);
-  return min(mf2_span_at(mf2_spans(M), pm) * kMf2Span, M);
+  return min(bnd[2 * SFM_MAX_BATCH + b] * kMf2Span, M);
+}
+
+// k_mf2_split (one block per pair), after the first launch (spans [0, sA),
+// sA = spans * pm / 1000): the pair's inlier ratio estimated from its largest
+// partial count, rho = max_c count(c) / nA, sets where the pruning happens.
+// A candidate with inlier ratio r can only be dropped after a share f of the
+// points with f (1 - r) > 1 - rho (its outliers so far must exceed every
+// point the winner does not hold), so the pruning point is f = 1 - rho +
+// margin (per mille; at least pm, and no pruning -- all spans before it --
+// when f would pass 990): 0.88 on the KITTI bench pairs (rho ~ 0.145), 0.92
+// on the indoor ones (rho ~ 0.105), where the fixed 0.88 of the first round-5
+// build could drop nothing and cost an extra launch boundary.  Writes the
+// boundaries bnd[0..3][b] = 0, sA, sB, spans for the launches A [0, sA), B
+// [sA, sB) (every candidate) and, after k_mf2_lead / k_mf2_keep at sB, C
+// [sB, spans) (the kept candidates).
+__global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int pm, int margin,
+                                                   const int32_t* __restrict__ cand_total,
+                                                   const int32_t* __restrict__ cntT, int32_t* __restrict__ bnd) {
+  __shared__ int s_max[16];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int M = max(pp.test[b], pp.rtest[b]);
+  const int all = mf2_spans(M);
+  const int sA = mf2_span_at(all, pm);
+  const int nA = min(sA * kMf2Span, M);
+  const int ctot = cand_total[b];
+  const int32_t* cnt = cntT + (size_t)b * cmax;
+  int mx = 0;
+  for (int c = tid; c < ctot; c += 1024) mx = max(mx, cnt[c]);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
+  if (lane == 0) s_max[wv] = mx;
+  __syncthreads();
+  if (tid != 0) return;
+  for (int w = 0; w < 16; ++w) mx = max(mx, s_max[w]);
+  // f = 1 - rho + margin in per mille, rounded up; >= pm; > 990: no pruning
+  const long long rho_pm = nA > 0 ? ((long long)mx * 1000) / nA : 0;
+  long long f = 1000 - rho_pm + margin;
+  f = max(f, (long long)pm);
+  const int sB = f > 990 ? all : max(sA, mf2_span_at(all, (int)f));
+  bnd[0 * SFM_MAX_BATCH + b] = 0;
+  bnd[1 * SFM_MAX_BATCH + b] = sA;
+  bnd[2 * SFM_MAX_BATCH + b] = sB;
+  bnd[3 * SFM_MAX_BATCH + b] = all;
 }
 
 template <class Src>
-__global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp, int cmax, int pm,
+__global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp, int cmax, const int32_t* __restrict__ bnd,
                                                   const int32_t* __restrict__ cand_total,
                                                   const double* __restrict__ candE, const int32_t* __restrict__ cntT,
                                                   ScoreConsts kc, int32_t* __restrict__ lead) {
@@ -470,7 +518,7 @@ __global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp,
   __shared__ int s_part[16];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int M = max(pp.test[b], pp.rtest[b]);
-  const int n1 = mf2_n1(pp, b, pm);
+  const int n1 = mf2_n1(pp, b, bnd);
   const int ctot = cand_total[b];
   if (ctot <= 0) return;
   const int32_t* cnt = cntT + (size_t)b * cmax;
@@ -513,7 +561,7 @@ __global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp,
   }
 }
 
-__global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, int pm,
+__global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, const int32_t* __restrict__ bnd,
                                                   const int32_t* __restrict__ cand_total,
                                                   const int32_t* __restrict__ cntT, int32_t* __restrict__ lead,
                                                   int32_t* __restrict__ cmap, unsigned long long* __restrict__ skipped) {
@@ -524,7 +572,7 @@ __global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, int 
   const int c0 = blockIdx.x * 1024;
   if (c0 >= ctot) return;
   const int M = max(pp.test[b], pp.rtest[b]);
-  const int n1 = mf2_n1(pp, b, pm);
+  const int n1 = mf2_n1(pp, b, bnd);
   const long long lb = (long long)lead[0 * SFM_MAX_BATCH + b] + lead[2 * SFM_MAX_BATCH + b];
   const int32_t* cnt = cntT + (size_t)b * cmax;
   auto kept = [&](int c) { return (long long)(M - n1) + cnt[c] >= lb; };

@@ -440,14 +440,18 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     (span, 32-candidate tile) units (64)
  *     "score_mf_chunk2"       0..4096 the same for the pruned second launch (0: as
  *                                     score_mf_chunk)
- *     "score_mf_prune"        0, 500..990  count-bound pruning in k_score_mf2 (880):
+ *     "score_mf_prune"        0, 500..990  count-bound pruning in k_score_mf2 (850):
  *                                     every candidate scored on the first N per
  *                                     mille of each pair's 1024-point spans, then
- *                                     only candidates whose bound can still reach
- *                                     the leader's exact count (k_mf2_lead / _keep); 0 =
- *                                     one launch.  Winner, count, E, P unchanged;
- *                                     only with num_test == num_ransac_test, no
- *                                     per-hypothesis scores, >= 32 spans per pair
+ *                                     up to the pair's pruning point 1 - (inlier
+ *                                     ratio estimated from them) + margin
+ *                                     (k_mf2_split), then only candidates whose
+ *                                     bound can still reach the leader's exact
+ *                                     count (k_mf2_lead / _keep); 0 = one launch.
+ *                                     Winner, count, E, P unchanged; only with
+ *                                     num_test == num_ransac_test, no per-
+ *                                     hypothesis scores, >= 32 spans per pair
+ *     "score_mf_prune_margin" 0..200  that margin, per mille (25)
  *     "roots_split"           0, 1, 2 k_roots_split: falsi nodes shared by the wave's
  *                                     64 lanes (1, default), or by the four waves of
  *                                     a block (2, measured 2-6 % slower), speculated

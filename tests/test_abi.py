@@ -156,7 +156,7 @@ def test_tuning_keys_round_trip():
     block = doc[doc.index("Tuning knobs"):doc.index("int sfm_tune_set")]
     keys = re.findall(r'"([a-z0-9_]+)"', block)
     assert set(keys) == set(_lib.tune_keys())           # documented == exported (sfm_tune_key)
-    assert len(set(keys)) == 27 and "score_mf_prune" in keys and "score_lowp_template" in keys
+    assert len(set(keys)) == 28 and "score_mf_prune" in keys and "score_lowp_template" in keys
     for k in keys:
         _lib.tune_get(k)
     old = _lib.tune_get("sweep_nj")
@@ -171,7 +171,7 @@ def test_tuning_keys_round_trip():
     with pytest.raises(Exception):
         _lib.tune_get("no_such_knob")
     snap = _lib.tune_snapshot()
-    assert snap["score_mf"] == 2 and snap["score_mf_prune"] == 880 and snap["score_mf_chunk"] == 64
+    assert snap["score_mf"] == 2 and snap["score_mf_prune"] == 850 and snap["score_mf_chunk"] == 64
     _lib.tune_restore(snap)
     assert _lib.load().sfm_tune_key(-1) is None and _lib.last_scorer() == ""
 

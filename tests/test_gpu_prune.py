@@ -1,9 +1,11 @@
 """Exact count-bound pruning, in both scorers that have it:
 
   * k_score_mf2 (the default and benched scorer; tuning key score_mf_prune):
-    every candidate scored on the first 880 per mille of each pair's spans,
-    k_mf2_lead / k_mf2_keep keep the candidates whose bound can still reach the leader's
-    exact count, a second launch scores those on the rest;
+    every candidate scored on the first 850 per mille of each pair's spans,
+    then up to the pair's pruning point (k_mf2_split: 1 - estimated inlier
+    ratio + margin), k_mf2_lead / k_mf2_keep keep the candidates whose bound
+    can still reach the leader's exact count, a last launch scores those on
+    the rest;
   * k_score32 (the float32 VALU scorer, score_mf=0; tuning key score_prune,
     PruneState).
 
@@ -32,7 +34,7 @@ def _both(pts, n=None, iters=2, thr=1e-4, nt=None, nr=None, scorer="mf2"):
         _lib.tune("score_mf", 2 if scorer == "mf2" else 0)
         for prune in (0, 1):
             if scorer == "mf2":
-                _lib.tune("score_mf_prune", 880 if prune else 0)
+                _lib.tune("score_mf_prune", 850 if prune else 0)
             else:
                 _lib.tune("score_prune", prune)
             E, P, inl, win = ransac.ransac5_batched(pts, n, nt, nr, iters, thr, workspace=ws)
@@ -86,14 +88,16 @@ def test_mf2_pruning_full_size_vs_oracle(cuda):
     assert skipped > 0.03 * total
 
 
-@pytest.mark.parametrize("pm", [500, 800, 990])
-def test_mf2_pruning_split_points(cuda, pm):
-    """Other first-launch shares (the key's range): the same results."""
+@pytest.mark.parametrize("pm,margin", [(500, 25), (800, 0), (990, 25), (850, 200), (600, 100)])
+def test_mf2_pruning_split_points(cuda, pm, margin):
+    """Other first-launch shares and margins (the keys' ranges, including a
+    pruning point past 990: no pruning): the same results."""
     from sfm_amd import _lib, ransac, synth
     flow, K, _, _ = synth.kitti_pair_batch(1, seed=5, hw=(200, 400), device=cuda)
     pts = ransac.flow_to_points(flow, torch.inverse(K))
     ref = ransac.ransac5_batched(pts, None, None, None, 2, 1e-3, return_scores=True)
     _lib.tune("score_mf_prune", pm)
+    _lib.tune("score_mf_prune_margin", margin)
     got = ransac.ransac5_batched(pts, None, None, None, 2, 1e-3)
     assert _lib.last_scorer() == "k_score_mf2+prune"
     for x, y in zip(got, ref[:4]):
@@ -150,3 +154,19 @@ def test_pruning_off_when_prefixes_differ(cuda, scorer):
     assert not kernels[1].endswith("+prune")
     _same(out)
     assert out[1][4] == 0
+
+
+def test_mf2_pruning_adapts_to_the_indoor_inlier_ratio(cuda):
+    """C4's indoor pairs hold ~10.5 % inliers: no candidate can be dropped
+    before 1 - 0.105 of the points, so a fixed pruning point at 0.88 dropped
+    nothing (round-5 first build); k_mf2_split moves it to ~0.92 and the
+    pruned launch skips evaluations there too, with the same results."""
+    from sfm_amd import ransac, synth
+    flow, K, _, _ = synth.kitti_pair_batch(2, seed=1000, hw=synth.INDOOR_HW, device=cuda, k=synth.INDOOR_K)
+    pts = ransac.flow_to_points(flow, torch.inverse(K), synth.INDOOR_HW[0], synth.INDOOR_HW[1])
+    out, kernels = _both(pts, iters=4)
+    assert kernels[1] == "k_score_mf2+prune"
+    _same(out)
+    N = pts.shape[1]
+    assert 0.05 < int(out[1][2].max()) / N < 0.12                 # the regime the test is about
+    assert out[1][4] > 0
