@@ -171,7 +171,7 @@ def test_tuning_keys_round_trip():
     with pytest.raises(Exception):
         _lib.tune_get("no_such_knob")
     snap = _lib.tune_snapshot()
-    assert snap["score_mf"] == 2 and snap["score_mf_prune"] == 850 and snap["score_mf_chunk"] == 64
+    assert snap["score_mf"] == 2 and snap["score_mf_prune"] == 880 and snap["score_mf_chunk"] == 64
     _lib.tune_restore(snap)
     assert _lib.load().sfm_tune_key(-1) is None and _lib.last_scorer() == ""
 

@@ -1,7 +1,7 @@
 """Exact count-bound pruning, in both scorers that have it:
 
   * k_score_mf2 (the default and benched scorer; tuning key score_mf_prune):
-    every candidate scored on the first 850 per mille of each pair's spans,
+    every candidate scored on the first 880 per mille of each pair's spans,
     then up to the pair's pruning point (k_mf2_split: 1 - estimated inlier
     ratio + margin), k_mf2_lead / k_mf2_keep keep the candidates whose bound
     can still reach the leader's exact count, a last launch scores those on
@@ -34,7 +34,7 @@ def _both(pts, n=None, iters=2, thr=1e-4, nt=None, nr=None, scorer="mf2"):
         _lib.tune("score_mf", 2 if scorer == "mf2" else 0)
         for prune in (0, 1):
             if scorer == "mf2":
-                _lib.tune("score_mf_prune", 850 if prune else 0)
+                _lib.tune("score_mf_prune", 880 if prune else 0)
             else:
                 _lib.tune("score_prune", prune)
             E, P, inl, win = ransac.ransac5_batched(pts, n, nt, nr, iters, thr, workspace=ws)
