@@ -281,10 +281,10 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
             t = done * FLOP_PER_EVAL / (rocprof[0] * 1e-3) / 1e12
             rp = {"avg_launch_ms": round(rocprof[0], 4), "achieved": round(t, 3),
                   "frac": round(t / PEAK_F16_TFLOPS, 4), "source": rocprof[1],
-                  "note": "k_mf_cands + k_score_mf2 (+ k_mf2_lead + k_mf2_keep) per step from the committed rocprofv3 --stats "
+                  "note": "k_mf_cands + k_score_mf2 (+ k_mf2_split + k_mf2_lead + k_mf2_keep) per step from the committed rocprofv3 --stats "
                           "summary of this workload (a profiled run clocks lower than this one)"}
         pruned = scorer == "k_score_mf2+prune"
-        kern = ("ransac_score (k_mf_cands + k_score_mf2 x2 + k_mf2_lead + k_mf2_keep: count-bound pruning)" if pruned
+        kern = ("ransac_score (k_mf_cands + k_score_mf2 x3 + k_mf2_split + k_mf2_lead + k_mf2_keep: count-bound pruning)" if pruned
                 else "ransac_score (k_mf_cands + k_score_mf2)")
         return {"kernel": kern, "scorer": scorer, "bound": "mfma-f16", "achieved": round(tflops, 3),
                 "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_F16_TFLOPS, 4),
@@ -603,7 +603,7 @@ def _main_gpu(args, dist):
             "roofline": score_roofline(use_mf, score_tflops, done, evals, skipped, sum(cands), hp.n, score_ms,
                                        traffic.get("ransac_score"), traffic_src,
                                        rocprof_kernel_ms(args, ("k_mf_cands", "k_score_mf2"),
-                                                         optional=("k_mf2_lead", "k_mf2_keep")), _lib.last_scorer()),
+                                                         optional=("k_mf2_split", "k_mf2_lead", "k_mf2_keep")), _lib.last_scorer()),
             "roofline_sweep": {"kernel": "plane_sweep", "bound": "hbm", "achieved": round(sweep_gbs, 1),
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(sweep_gbs / PEAK_HBM_GBS, 4),
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,

@@ -52,7 +52,7 @@ WORKLOADS = {"c2": (8, 8, 128, "fp32"), "c3": (4, 8, 128, "bf16"), "c4": (8, 4, 
 def main(src, dst, config="c2"):
     # per (path key, kernel): one list of per-dispatch values per counter.  A
     # path key can hold several kernels of one step (ransac_score = k_mf_cands
-    # + 2 x k_score_mf2 + k_mf2_lead + k_mf2_keep with pruning): its per-step
+    # + k_score_mf2 launches + k_mf2_split + k_mf2_lead + k_mf2_keep with pruning): its per-step
     # figure is the SUM of all their dispatches per step
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True)):
@@ -71,7 +71,7 @@ def main(src, dst, config="c2"):
         m = collections.defaultdict(float)
         # per step: every dispatch of the key's kernels summed over the steps,
         # the step count being the fewest dispatches of any of them (k_mf_cands
-        # once per step; the pruned scorer launches k_score_mf2 twice)
+        # once per step; the pruned scorer launches k_score_mf2 three times)
         steps = min(max(len(v) for v in per[(k, name)].values()) for name in names)
         for name in names:
             for c, v in per[(k, name)].items():

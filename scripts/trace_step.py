@@ -3,7 +3,7 @@ duration and the gap before it (usage: trace_step.py run_kernel_trace.csv)."""
 import csv
 import sys
 
-NAMES = ["k_mf_cands", "k_score_mf2", "k_mf2_lead", "k_mf2_keep", "k_select", "k_sweep_tile", "k_tgt_quads",
+NAMES = ["k_mf_cands", "k_score_mf2", "k_mf2_split", "k_mf2_lead", "k_mf2_keep", "k_select", "k_sweep_tile", "k_tgt_quads",
          "k_cand", "k_chain", "k_solve_back", "k_roots_split", "k_solve_front", "k_flow_points", "k_kinv3"]
 
 

@@ -155,16 +155,17 @@ def test_rocprof_kernel_match_is_whole_name(tmp_path, monkeypatch):
     ms, src = bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf2"))
     assert abs(ms - 5.01) < 1e-9 and src.endswith("r09_kernel_stats_v1.csv")
     assert bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf"))[0] is None
-    # the pruned scorer: two k_score_mf2 launches, k_mf2_lead and k_mf2_keep per step
+    # the pruned scorer: k_score_mf2 launches, k_mf2_split, k_mf2_lead and k_mf2_keep per step
     (prof / "r09_kernel_stats_v3.csv").write_text(
         '"Name","Calls","TotalDurationNs","AverageNs"\n'
         '"_ZN3sfm11k_score_mf2INS_9PackedSrcEEEvT_",4,10000000,2500000\n'
         '"_ZN3sfm10k_mf2_leadINS_9PackedSrcEEEvT_",2,30000,15000\n'
         '"_ZN3sfm10k_mf2_keepENS_10PairParamsEii",2,10000,5000\n'
+        '"_ZN3sfm11k_mf2_splitENS_10PairParamsEii",2,8000,4000\n'
         '"_ZN3sfm10k_mf_candsEiPKi",2,20000,10000\n')
     (prof / "r09_kernel_stats_v3.meta.json").write_text(json.dumps({"src_hash": "cur"}))
-    ms, src = bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf2"), optional=("k_mf2_lead", "k_mf2_keep"))
-    assert abs(ms - 5.03) < 1e-9 and src.endswith("r09_kernel_stats_v3.csv")
+    ms, src = bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf2"), optional=("k_mf2_split", "k_mf2_lead", "k_mf2_keep"))
+    assert abs(ms - 5.034) < 1e-9 and src.endswith("r09_kernel_stats_v3.csv")
     monkeypatch.setattr(bench, "src_hash", lambda: "new")
     assert bench.rocprof_kernel_ms(A, ("k_mf_cands", "k_score_mf2")) == (None, None)
 
