@@ -1567,21 +1567,21 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
       // k_mf2_keep; C the kept candidates on the rest
       const int ch = tuning().score_mf_chunk;
       const int ch2 = tuning().score_mf_chunk2 ? tuning().score_mf_chunk2 : ch;
-      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
+      hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
                          kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr, 0, ch);
       hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, prune_pm, tuning().score_mf_prune_margin,
                          w.cand_total, w.cntT, w.bnd);
-      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
+      hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
                          kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
       hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
                          (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead);
       hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax,
                          (const int32_t*)w.bnd, w.cand_total, w.cntT, w.lead, w.cmap, w.skipped);
-      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH, w.candE,
+      hipLaunchKernelGGL((k_score_mf2<Src, true>), g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH, w.candE,
                          w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap, 0, 0, (const int32_t*)w.bnd, 2, ch2);
       set_last_scorer("k_score_mf2+prune");
     } else if (same && tuning().score_mf == 2) {
-      hipLaunchKernelGGL(k_score_mf2<Src>, g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
+      hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
                          kc, w.claim, (const int32_t*)nullptr, 0, 1000, (const int32_t*)nullptr, 0,
                          tuning().score_mf_chunk);
       set_last_scorer("k_score_mf2");

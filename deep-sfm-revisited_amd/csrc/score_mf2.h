@@ -153,11 +153,11 @@ __device__ __forceinline__ int32_t* mf2_count_slot(int32_t* cntT, const int32_t*
   return cntT + (size_t)b * cmax + (cmap ? cmap[i] : j);
 }
 
-template <class Src>
+template <class Src, bool kMap>
 __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(kMf2Wpe, kMf2Wpe))) void k_score_mf2(
     const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
     const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
-    ScoreConsts kc, unsigned long long* __restrict__ claim, const int32_t* __restrict__ cmap, int sp_lo,
+    ScoreConsts kc, unsigned long long* __restrict__ claim, const int32_t* __restrict__ cmap_arg, int sp_lo,
     int sp_hi, const int32_t* __restrict__ bnd, int phase, int min_chunk) {
   // one count array: this kernel runs only when num_test == num_ransac_test,
   // so the preselection count is the score and k_select reads cntT for both
@@ -172,6 +172,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   __shared__ int32_t s_span0[SFM_MAX_BATCH];                 // the pair's first span in this launch
   __shared__ int32_t s_claim;                                // next candidate tile of the span to claim
   __shared__ long long s_range[2];                           // the block's current unit range
+  // the compacted candidates' index map: a compile-time null in the launches
+  // without one, so that its address arithmetic costs the tile loop no registers
+  const int32_t* __restrict__ const cmap = kMap ? cmap_arg : nullptr;
   const int tid = threadIdx.x, wv = tid >> 6;
   if (tid == 0) {
     long long acc = 0;
