@@ -1033,14 +1033,12 @@ __device__ __forceinline__ void enqueue_undecided(uint64_t und, int c, int p, in
     atomicAdd(&g_score_stats[2], (unsigned long long)__popcll(und));
   }
 #endif
-#ifndef SFM_SCORE_NOFALLBACK
   if (!und) return;                                     // wave-uniform
   if ((und >> lane) & 1ull) {
     const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(und >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)und, 0));
     q[pos] = ((uint32_t)c << 24) | (uint32_t)p;
   }
   qn += __popcll(und);
-#endif
 }
 
 // One float32 pass of a wave over candidates [c, nc) of its chunk (lane l
@@ -1295,18 +1293,14 @@ void k_score32(const Src src, PairParams pp, int batch, int cmax, const int32_t*
         }
         c = __builtin_amdgcn_readfirstlane(c);
         if (c >= nc) break;
-#ifndef SFM_SCORE_NOFALLBACK
         wave_sync();                                      // queue past its low mark: drain, resume at c
         score32_drain(CE, src, b, p0, T, R, kc, lane, cnt, queue, qn);
         qn = 0;
         wave_sync();
-#endif
       }
     }
-#ifndef SFM_SCORE_NOFALLBACK
     wave_sync();
     score32_drain(CE, src, b, p0, T, R, kc, lane, cnt, queue, qn);
-#endif
     wave_sync();
     if (kc.prune) {
       // publish (count, covered) of the span; raise the pair's best count so far

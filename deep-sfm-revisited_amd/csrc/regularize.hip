@@ -32,9 +32,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kTileX = 64;          // output columns per block
 constexpr int kXcds = 8;            // MI355X: 8 XCDs, each with its own L2
-#ifndef SFM_CONV_EXP
-#define SFM_CONV_EXP 0  // timing-experiment builds only (scripts/build_exp.sh); 0 in the product
-#endif
 #ifndef SFM_CONV_MINW
 #define SFM_CONV_MINW 2
 #endif
@@ -453,20 +450,8 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
     __syncthreads();
     if (j + 1 < nsteps) fetch(d0 + j);  // plane of step j + 1
     const bool v0 = j < nd, v1 = j >= 1 && j - 1 < nd, v2 = j >= 2;
-#if SFM_CONV_EXP == 3  // timing experiment: operands read once per plane, not per group (wrong results)
-    v8 wf[3][3], xf[4];
-#pragma unroll
-    for (int dz = 0; dz < 3; ++dz)
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy)
-        wf[dz][dy] = *reinterpret_cast<const v8*>(lds_w + (((dz * 3 + dy) * 3) * 32 + r) * 64 + swz(h, r) * 16);
-#pragma unroll
-    for (int ir = 0; ir < 4; ++ir)
-      xf[ir] = *reinterpret_cast<const v8*>(lds_in + ((wrow + ir) * kHaloX + wcol + r) * 64 + swz(h, wcol + r) * 16);
-#endif
 #pragma unroll
     for (int g = 0; g < 6; ++g) {
-#if SFM_CONV_EXP != 3
       const int kb = g / 3, dx = g - 3 * (g / 3);
       const int c = kb * 2 + h;
       v8 wf[3][3], xf[4];
@@ -479,7 +464,6 @@ __global__ __launch_bounds__(256, 2) void k_conv3r(const unsigned short* __restr
 #pragma unroll
       for (int ir = 0; ir < 4; ++ir)
         xf[ir] = *reinterpret_cast<const v8*>(lds_in + ((wrow + ir) * kHaloX + p) * 64 + swz(c, p) * 16);
-#endif
       if (v0) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)

@@ -905,12 +905,7 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
         }
         if (in) acc[n][j] = a;
       }
-#ifdef SFM_SWEEP_EXP_NOSAMPLE
-    // experiment builds only: the sample at the pixel itself (no projection)
-    } else if ((ix = xf + 0.25f * d * 1e-9f, iy = yf, true)) {
-#else
     } else if (sample_pos_nr(pr, ray, d, sk, ix, iy)) {
-#endif
       TapsIn tp;
       make_taps_inside(ix, iy, g.h, g.w, tp);
 #pragma unroll
@@ -919,12 +914,7 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
         f32x4 t[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-#ifdef SFM_SWEEP_EXP_NOGATHER
-          // experiment builds only (what binds the sweep): no tap gathers
-          t[e] = f32x4{tp.wt[e], tp.wt[e] + 1.0f, __uint_as_float(tp.off[e]), (float)n};
-#else
           t[e] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rtq, tp.off[e] * 16u, so, 0));
-#endif
         f32x4 a;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -974,23 +964,9 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[kSwThreads / 64][RPS][16 * LPR / 4];
     const int rr = lane / LPR, cl = lane - rr * LPR;
     const unsigned voff = (unsigned)(woff + EPL * cl) * (unsigned)sizeof(OutT) + (unsigned)rr * row_bytes;
-    // (per-pixel LDS writes: staging the plain path's DPP-packed bf16 pairs as
-    // 4-byte writes gave wrong words at upper-half chunk starts on gfx950 --
-    // scripts/diag_wide.py; the cause was not isolated)
+    // (per-pixel LDS writes; the DPP-packed pairs staged as 4-byte writes are
+    // equally correct since the store-hazard fix below, profiles/r05_store_hazard.txt)
     auto put = [&](int slot, const float* v) {
-#ifdef SFM_SWEEP_PAIRSTAGE
-      // experiment builds only (round 5, the round-4 miscompute): the plain
-      // path's DPP-packed bf16 pairs staged as 4-byte LDS writes
-      if constexpr (BF) {
-        uint32_t* st32 = s_rows[wave][slot];
-#pragma unroll
-        for (int s = 0; s < NJ / 2; ++s) {
-          const unsigned u = bf16_pair_swap(to_bf16(v[2 * s]), to_bf16(v[2 * s + 1]), odd);
-          st32[(128 * s + lane + (odd ? 63 : 0)) >> 1] = u;
-        }
-        return;
-      }
-#endif
       OutT* st = reinterpret_cast<OutT*>(s_rows[wave][slot]);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -1001,18 +977,6 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
     auto flush = [&](unsigned r0) {             // rows r0 .. r0 + RPS - 1
       sweep_wave_sync();
       const u32x4 x = *reinterpret_cast<const u32x4*>(&s_rows[wave][rr][4 * cl]);
-#ifdef SFM_SWEEP_STORE_NOP
-      // experiment builds only: the store and one wait state as one asm block
-      if (NT)
-        asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen sc0 nt\n\ts_nop 0"
-                     :: "v"(x), "v"(voff), "s"(rout), "s"(r0 * row_bytes) : "memory");
-      else
-        asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 0"
-                     :: "v"(x), "v"(voff), "s"(rout), "s"(r0 * row_bytes) : "memory");
-#elif defined(SFM_SWEEP_SGPR_SOFFSET)
-      // experiment builds only: the round-4 form (row offset as the SGPR soffset)
-      __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff, r0 * row_bytes, NT ? 3 : 0);
-#else
       // the row offset in voffset with a literal-0 soffset, not an SGPR
       // soffset: a 128-bit store's data VGPRs must not be overwritten by the
       // next instruction (gfx950 stores the new value for lanes 16r+12..15
@@ -1021,7 +985,6 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       // soffset -- the round-4 "4-byte staging miscompute" was this pair
       // (profiles/r05_store_hazard.txt)
       __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff + r0 * row_bytes, 0, NT ? 3 : 0);
-#endif
       sweep_wave_sync();                        // the stage's reads before the next rows' writes
     };
     static_assert(G % RPS == 0, "row groups");

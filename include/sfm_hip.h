@@ -438,7 +438,7 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     2 by default; exact by proof, same counts)
  *     "score_mf_chunk"        1..4096 k_score_mf2's smallest claimed unit range, in
  *                                     (span, 32-candidate tile) units (64)
- *     "score_mf_chunk2"       0..4096 the same for the pruned second launch (0: as
+ *     "score_mf_chunk2"       0..4096 the same for the pruned sequence's last launch (0: as
  *                                     score_mf_chunk)
  *     "score_mf_prune"        0, 500..990  count-bound pruning in k_score_mf2 (880):
  *                                     every candidate scored on the first N per

@@ -3,7 +3,6 @@
 # csrc/Makefile); never used by the product, selected with SFM_HIP_LIB.
 # With no arguments builds the standard set:
 #   STATS       score-kernel undecided statistics   (scripts/score_experiment.py)
-#   NOFALLBACK  score kernel without the float64 re-tests (timing only; wrong counts)
 #   SOLVESTATS  per-phase cycle counters of k_solve  (scripts/solve_experiment.py)
 # or NAME=FLAGS pairs, e.g.  scripts/build_exp.sh "P6W6=-DSFM_PPL32=6 -DSFM_SCORE_WAVES=6"
 set -e
@@ -17,7 +16,6 @@ build() {
 }
 if [ $# -eq 0 ]; then
   build STATS -DSFM_SCORE_STATS
-  build NOFALLBACK -DSFM_SCORE_NOFALLBACK
   build SOLVESTATS -DSFM_SOLVE_STATS
 else
   for spec in "$@"; do
