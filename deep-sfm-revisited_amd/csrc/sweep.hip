@@ -93,7 +93,8 @@ __device__ __forceinline__ void psnet_prep_pair(const PsnetPrep& q, int B, int b
 __global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4, int hw, f32x4* __restrict__ tq,
                             const float* __restrict__ pose, const float* __restrict__ K4,
                             const float* __restrict__ K4inv, Proj* __restrict__ projs, int L, float dmax,
-                            float dstep, float* __restrict__ depths, PsnetPrep prep) {
+                            float dstep, float* __restrict__ depths, PsnetPrep prep,
+                            const float* __restrict__ ref = nullptr, unsigned short* __restrict__ ref16 = nullptr) {
   // grid (pixels, quads, pairs): no integer division per thread; the uniform
   // per-pair and per-plane tables from the first quad row of pair 0
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -122,6 +123,15 @@ __global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4,
     v[k] = c < C ? tgt[((size_t)b * C + c) * hw + i] : 0.0f;
   }
   tq[((size_t)b * C4 + q) * hw + i] = v;
+  if (ref16) {
+    // a bf16 volume's reference rows, converted once (k_sweep_tile's 16-byte
+    // stores copy them from here instead of converting per plane)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * q + k;
+      if (c < C) ref16[((size_t)b * C + c) * hw + i] = to_bf16(ref[((size_t)b * C + c) * hw + i]);
+    }
+  }
 }
 
 static dim3 quads_grid(int B, int C4, int hw, int extra) {
@@ -391,6 +401,8 @@ struct FlatGeom {
   float inv_w;
   float dmax, dstep;
   const float* depths;   // plane depths (k_tgt_quads), or null
+  const unsigned short* ref16;   // bf16 volumes: the reference rows in bf16 [B][C][hw] (k_tgt_quads), or null
+  int wpol;        // 16-byte stores' cache policy when not -1 (16 sc1, 17 sc0 sc1, 18 nt sc1; sweep_store_wt)
 };
 
 template <typename OutT> struct FlatLanes;   // pixels per lane per store, stores per lane per row
@@ -787,7 +799,7 @@ __device__ __forceinline__ unsigned next_lane_u(unsigned v) {
 }
 __device__ __forceinline__ float next_lane_f(float v) { return __uint_as_float(next_lane_u(__float_as_uint(v))); }
 
-template <typename OutT, int NQ, int NJ, bool SHARE, bool NT, bool WIDE = false>
+template <typename OutT, int NQ, int NJ, bool SHARE, bool NT, bool WIDE = false, int WPOL = -1>
 __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, const f32x4* __restrict__ tq,
                                                 const Proj* __restrict__ projs, const FlatGeom& g,
                                                 OutT* __restrict__ out, int b, int k, int start) {
@@ -822,8 +834,10 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
           __builtin_amdgcn_raw_buffer_load_b32(rref, (unsigned)ps[j] * 4u, (unsigned)c * g.hw * 4u, 0));
   };
   constexpr bool LATE = WIDE && NJ == 8;        // registers: the reference rows at their stores
+  // bf16 wide stores with the converted reference rows: copied at their stores
+  const bool r16 = WIDE && BF && g.ref16 != nullptr;
   float cp[LATE ? 1 : G][NJ];
-  if (!LATE && g.ref_rows && g.write_ref) {
+  if (!LATE && !r16 && g.ref_rows && g.write_ref) {
 #pragma unroll
     for (int c = 0; c < G; ++c) load_ref_row(c, cp[LATE ? 0 : c]);
   }
@@ -960,6 +974,10 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
     // rows (1 KB) at their window positions and come back as EPL consecutive
     // pixels per lane; the tap gathers stay lane-consecutive.
     constexpr int EPL = 16 / (int)sizeof(OutT), LPR = 64 * NJ / EPL, RPS = 64 / LPR;
+    // the 16-byte stores' cache policy: sc0 nt / plain by NT, or WPOL (sc1:
+    // write-through, the line is not kept in the XCD's L2 -- tuning key
+    // sweep_store_wt)
+    constexpr int POL = WPOL >= 0 ? WPOL : (NT ? 3 : 0);
     static_assert(NJ <= EPL && EPL % NJ == 0, "wide stores: NJ divides the pixels of a 16-byte store");
     __shared__ __attribute__((aligned(16))) uint32_t s_rows[kSwThreads / 64][RPS][16 * LPR / 4];
     const int rr = lane / LPR, cl = lane - rr * LPR;
@@ -984,7 +1002,7 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       // recognizer inserts that wait state only for stores without an SGPR
       // soffset -- the round-4 "4-byte staging miscompute" was this pair
       // (profiles/r05_store_hazard.txt)
-      __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff + r0 * row_bytes, 0, NT ? 3 : 0);
+      __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff + r0 * row_bytes, 0, POL);
       sweep_wave_sync();                        // the stage's reads before the next rows' writes
     };
     static_assert(G % RPS == 0, "row groups");
@@ -999,7 +1017,34 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       }
       flush((unsigned)(g.ref_rows + c0 + c));
     }
-    if (g.ref_rows && g.write_ref) {
+    if (g.ref_rows && g.write_ref && r16) {
+      // the reference rows straight from their bf16 copy: lane (rr, cl)
+      // loads the EPL pixels it stores (plane l0's or, past its end, the next
+      // plane's pixel offsets; a chunk across the plane boundary by element)
+      const __amdgpu_buffer_rsrc_t r16r =
+          buf_rsrc(g.ref16 + ((size_t)b * g.C + c0) * g.hw, (unsigned)G * g.hw * 2u);
+      int p0 = woff + EPL * cl - l0 * g.hw;
+      while (p0 >= g.hw) p0 -= g.hw;
+      const bool wrap = p0 + EPL > g.hw;
+#pragma unroll
+      for (int c = 0; c < G; c += RPS) {
+        const unsigned so = (unsigned)(c + rr) * g.hw * 2u;
+        u32x4 x;
+        if (!wrap) {
+          x = __builtin_amdgcn_raw_buffer_load_b128(r16r, (unsigned)p0 * 2u, so, 0);
+        } else {
+          unsigned hv[EPL];
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) {
+            const int pe = p0 + e < g.hw ? p0 + e : p0 + e - g.hw;
+            hv[e] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(r16r, (unsigned)pe * 2u, so, 0);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = hv[2 * e] | (hv[2 * e + 1] << 16);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff + (unsigned)(c0 + c) * row_bytes, 0, POL);
+      }
+    } else if (g.ref_rows && g.write_ref) {
 #pragma unroll
       for (int c = 0; c < G; c += RPS) {
 #pragma unroll
@@ -1050,7 +1095,10 @@ __global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restri
   {
     if constexpr (NJ <= 16 / (int)sizeof(OutT)) {
       if (NJ == 8 || (g.store_px == NJ && !g.share)) {     // NJ = 8 is launched for wide stores only
-        if (g.store_nt) sweep_tile_fast<OutT, NQ, NJ, false, true, true>(ref, tq, projs, g, out, b, k, start);
+        if (g.wpol == 16) sweep_tile_fast<OutT, NQ, NJ, false, false, true, 16>(ref, tq, projs, g, out, b, k, start);
+        else if (g.wpol == 17) sweep_tile_fast<OutT, NQ, NJ, false, false, true, 17>(ref, tq, projs, g, out, b, k, start);
+        else if (g.wpol == 18) sweep_tile_fast<OutT, NQ, NJ, false, false, true, 18>(ref, tq, projs, g, out, b, k, start);
+        else if (g.store_nt) sweep_tile_fast<OutT, NQ, NJ, false, true, true>(ref, tq, projs, g, out, b, k, start);
         else sweep_tile_fast<OutT, NQ, NJ, false, false, true>(ref, tq, projs, g, out, b, k, start);
         return;
       }
@@ -1417,8 +1465,13 @@ static size_t sweep_proj_bytes(int B) { return ((size_t)B * sizeof(Proj) + 255) 
 // sfm_plane_sweep_psnet: float32 pose, K4, K4inv per pair (12 + 9 + 9 floats)
 static size_t sweep_psnet_bytes(int B) { return ((size_t)B * 30 * sizeof(float) + 255) & ~(size_t)255; }
 // what launch_sweep uses: quads, Proj table, plane depths
+// the bf16 copy of the reference rows (bf16 volumes with even h*w)
+static size_t sweep_ref16_bytes(int B, int C, int h, int w) {
+  return ((size_t)B * C * (size_t)h * w * sizeof(unsigned short) + 255) & ~(size_t)255;
+}
 static size_t sweep_core_bytes(int B, int C, int h, int w) {
-  return sweep_quads_bytes(B, C, h, w) + sweep_proj_bytes(B) + kDepthTable * sizeof(float);
+  return sweep_quads_bytes(B, C, h, w) + sweep_proj_bytes(B) + kDepthTable * sizeof(float) +
+         sweep_ref16_bytes(B, C, h, w);
 }
 // the public size: the core plus the sfm_plane_sweep_psnet operands at its end
 static size_t sweep_ws_bytes(int B, int C, int h, int w) { return sweep_core_bytes(B, C, h, w) + sweep_psnet_bytes(B); }
@@ -1460,10 +1513,15 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   f32x4* tq = (f32x4*)ws;
   Proj* projs = reinterpret_cast<Proj*>((char*)ws + sweep_quads_bytes(B, C, h, w));
   float* depths = L <= kDepthTable ? reinterpret_cast<float*>((char*)projs + sweep_proj_bytes(B)) : nullptr;
+  // bf16 volume with its reference rows and an even h*w (every plane's copy
+  // then starts 4-byte aligned): the rows are converted once here
+  unsigned short* ref16 = nullptr;
+  if (out_dtype == 1 && with_ref && write_ref && hw % 2 == 0 && tuning().sweep_ref16)
+    ref16 = reinterpret_cast<unsigned short*>((char*)projs + sweep_proj_bytes(B) + kDepthTable * sizeof(float));
   {
     ProfScope ps("sweep_tgt_quads", s);
     hipLaunchKernelGGL(k_tgt_quads, quads_grid(B, g.C4, hw, std::max(B, L)), dim3(256), 0, s, tgt, B, C, g.C4, hw, tq,
-                       pose, K4, K4inv, projs, L, g.dmax, g.dstep, depths, prep);
+                       pose, K4, K4inv, projs, L, g.dmax, g.dstep, depths, prep, ref, ref16);
   }
   SFM_LAUNCHED();
   const char* pname = with_ref ? "plane_sweep" : "plane_sweep_warped";
@@ -1482,10 +1540,10 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   // fp32: 1, 2, 4); rows keep 16-byte alignment from window to window (slab
   // a multiple of a store's pixels)
   // default (-1): bf16 volumes 2 pixels per lane (the C3 sweep 0.454 -> 0.347 ms
-  // in the bench step, profiles/r04_sweep_wide_ab.txt), fp32 the plain stores
-  // (write-bound already: 1 pixel per lane equal, 2 slower)
+  // in the bench step, profiles/r04_sweep_wide_ab.txt), fp32 1 pixel per lane
+  // (with the nt sc1 policy below; 2 pixels per lane are slower)
   int store_px = tuning().sweep_store_px;
-  if (store_px < 0) store_px = out_dtype == 1 ? 2 : 0;
+  if (store_px < 0) store_px = out_dtype == 1 ? 2 : 1;
   if (out_dtype == 1 && store_px == 1) store_px = 2;
   if (out_dtype == 0 && store_px == 8) store_px = 0;
   if (!(mode == 2 && slab % (out_dtype == 1 ? 8 : 4) == 0 && (uintptr_t)out % 16 == 0 && !tuning().sweep_share))
@@ -1565,6 +1623,17 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     fg.inv_w = 1.0f / (float)w;
     fg.dmax = g.dmax; fg.dstep = g.dstep;
     fg.depths = depths;
+    fg.ref16 = (mode == 2 && store_px) ? ref16 : nullptr;
+    {
+      // auto (-1): fp32 volumes nt sc1 (write-through: the volume's lines do
+      // not stay in the XCD's L2, where plain / nt stores keep them), bf16 by
+      // sweep_store_nt.  Measured (profiles/r05_sweep_store_wt.txt): inside the
+      // bench step the fp32 sweep 1.275 -> 1.245 ms (c2) and 0.440 -> 0.422 ms
+      // (c4); bf16 slower with sc1 (0.359 -> 0.384 ms, c3)
+      int wt = tuning().sweep_store_wt;
+      if (wt < 0) wt = out_dtype == 0 ? 3 : 0;
+      fg.wpol = wt == 1 ? 16 : wt == 2 ? 17 : wt == 3 ? 18 : -1;
+    }
     const unsigned blocks = (unsigned)((int64_t)B * fgroups * nwin);
     ProfScope ps(pname, s);
     if (mode == 2) {

@@ -417,11 +417,20 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     whose channel slab L*h*w*4 is <= 6 MiB --
  *                                     measured per shape, e.g. on for the indoor
  *                                     120x160 L=64 volume, off for KITTI 94x311)
+ *     "sweep_store_wt"        -1..3   cache policy of k_sweep_tile's 16-byte stores:
+ *                                     0 by sweep_store_nt, 1 sc1 (write-through:
+ *                                     the line is not kept in the XCD's L2), 2 sc0
+ *                                     sc1, 3 nt sc1; -1 (default): fp32 volumes 3,
+ *                                     bf16 volumes 0; same bits
+ *     "sweep_ref16"           0, 1    bf16 volumes with 16-byte stores and an even h*w:
+ *                                     the reference rows copied from a bf16 copy
+ *                                     k_tgt_quads makes once (1), not converted per plane
+ *                                     from the fp32 rows (0); same bits
  *     "sweep_store_px"        -1,0,1, 16-byte lane stores of k_sweep_tile (8 bf16 / 4
  *                             2,4,8   fp32 consecutive pixels through a per-wave LDS
  *                                     stage) with that many pixels per lane for the
  *                                     taps; 0: plain 4-byte lane stores; -1 (default):
- *                                     bf16 2, fp32 plain; same bits
+ *                                     bf16 2, fp32 1; same bits
  *     "sweep_run"             1..1024 planes per block of k_sweep_band (16)
  *     "sweep_band_rows"       2..64   target rows k_sweep_band stages in LDS (16,
  *                                     clipped to 80 KB per block)

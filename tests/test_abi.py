@@ -156,7 +156,7 @@ def test_tuning_keys_round_trip():
     block = doc[doc.index("Tuning knobs"):doc.index("int sfm_tune_set")]
     keys = re.findall(r'"([a-z0-9_]+)"', block)
     assert set(keys) == set(_lib.tune_keys())           # documented == exported (sfm_tune_key)
-    assert len(set(keys)) == 28 and "score_mf_prune" in keys and "score_lowp_template" in keys
+    assert len(set(keys)) == 30 and "score_mf_prune" in keys and "sweep_ref16" in keys and "score_lowp_template" in keys
     for k in keys:
         _lib.tune_get(k)
     old = _lib.tune_get("sweep_nj")
