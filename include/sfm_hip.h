@@ -424,8 +424,9 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     bf16 volumes 0; same bits
  *     "sweep_ref16"           0, 1    bf16 volumes with 16-byte stores and an even h*w:
  *                                     the reference rows copied from a bf16 copy
- *                                     k_tgt_quads makes once (1), not converted per plane
- *                                     from the fp32 rows (0); same bits
+ *                                     k_tgt_quads makes once (1; measured ~1 % slower),
+ *                                     or converted per plane from the fp32 rows (0,
+ *                                     default); same bits
  *     "sweep_store_px"        -1,0,1, 16-byte lane stores of k_sweep_tile (8 bf16 / 4
  *                             2,4,8   fp32 consecutive pixels through a per-wave LDS
  *                                     stage) with that many pixels per lane for the
