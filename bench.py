@@ -84,9 +84,13 @@ def parse(argv=None):
                          "MI355X pool (nproc there reports the whole 256-thread host)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="full-pair CPU baseline runs (median; BASELINE.md: >= 5)")
     ap.add_argument("--pipeline", action="store_true",
-                    help="each step's sweep on a side stream, overlapping the next step's pose stage "
-                         "(TwoViewHotPath.step_pipelined): c2 +1.7 %%, sparse +12 %% pairs/s, but the overlapped "
-                         "kernels' launch durations (the roofline fields) then include the overlap")
+                    help="each step's sweep on a side stream, overlapping the next step's pose stage, the "
+                         "next scorer held for it (TwoViewHotPath.step_pipelined, sfm_score_gate): round 5 c2 "
+                         "+0.2 %%, c4 / sparse +5 %%, c3 +0.6 %% pairs/s (profiles/r05_pipeline_gate_ab.txt); the "
+                         "overlapped kernels' launch durations (the roofline fields) then include the overlap")
+    ap.add_argument("--no-gate", action="store_true",
+                    help="with --pipeline: do not hold the next step's scorer for the side-stream sweep "
+                         "(sfm_score_gate); the sweep then overlaps the scorer too")
     ap.add_argument("--overlap-ref", default="0", choices=("0", "score", "step"),
                     help="the cost volume's pose-independent reference half on a side stream "
                          "(TwoViewHotPath.step_overlap): 'score' beside the RANSAC scorer (behind the score fence), "
@@ -512,7 +516,8 @@ def _main_gpu(args, dist):
     hp = TwoViewHotPath(B, hw, fhw, C, args.nlabel, args.iters, args.threshold, 1.0, rescale_depth=True,
                         norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused,
                         keypoints=None if kp is None else (kp, [args.keypoints] * B),
-                        overlap_ref=False if args.overlap_ref == "0" else args.overlap_ref)
+                        overlap_ref=False if args.overlap_ref == "0" else args.overlap_ref,
+                        gate_scorer=not args.no_gate)
 
     # --pipeline: step i's sweep (side stream) overlaps step i+1's pose stage
     stepf = hp.step_pipelined if args.pipeline else hp.step

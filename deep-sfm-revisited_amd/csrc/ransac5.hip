@@ -1749,6 +1749,24 @@ static int record_score_fence(hipStream_t s) {
   return SFM_OK;
 }
 
+// Score gate (sfm_score_gate): an event the next RANSAC call on a device
+// waits for right before its scoring phase (one-shot), so that a pipelined
+// caller can run the previous step's HBM-bound sweep beside this step's
+// latency-bound solve while keeping the compute-bound scorer to itself.
+static hipEvent_t g_gate[kFenceDevices] = {};
+
+static int wait_score_gate(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_fence_mu);
+  int dev = 0;
+  if (int rc = stream_device(s, &dev)) return rc;
+  if (g_gate[dev]) {
+    const hipEvent_t ev = g_gate[dev];
+    g_gate[dev] = nullptr;
+    SFM_HIP(hipStreamWaitEvent(s, ev, 0));
+  }
+  return SFM_OK;
+}
+
 template <class Src>
 static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
                      int num_ransac_test, int iters, double thr, uint64_t seed, int cheir,
@@ -1838,6 +1856,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     SFM_HIP(hipMemsetAsync(w.best_lb, 0, SFM_MAX_BATCH * kBestStride * 4, s));
   }
   if (int rc = record_score_fence(s)) return rc;
+  if (int rc = wait_score_gate(s)) return rc;
   {
     ProfScope ps("ransac_score", s);
     ScoreBufs sb{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim};
@@ -1980,6 +1999,14 @@ int sfm_score_fence_wait(void* stream) {
   hipEvent_t ev = nullptr;
   if (int rc = fence_of((hipStream_t)stream, &ev)) return rc;
   SFM_HIP(hipStreamWaitEvent((hipStream_t)stream, ev, 0));
+  return SFM_OK;
+}
+
+int sfm_score_gate(void* event, void* stream) {
+  std::lock_guard<std::mutex> lk(g_fence_mu);
+  int dev = 0;
+  if (int rc = stream_device((hipStream_t)stream, &dev)) return rc;
+  g_gate[dev] = (hipEvent_t)event;
   return SFM_OK;
 }
 

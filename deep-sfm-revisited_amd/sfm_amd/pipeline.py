@@ -14,6 +14,8 @@ branch of pose_by_ransac 176-274, and PSNet.py:130-158):
 All buffers (points, RANSAC workspace, cost volume) are allocated once and
 reused, so a step launches kernels only (hipGraph-capturable).
 """
+import ctypes
+
 import torch
 
 from . import _lib, ransac, sweep
@@ -38,8 +40,12 @@ def kinv3x3(K):
 class TwoViewHotPath:
     def __init__(self, batch, image_hw, feat_hw, channels=32, nlabel=128, iters=8, threshold=1e-4,
                  min_depth=1.0, rescale_depth=False, norm_target=0.6, cost_dtype=torch.float32, margin=10,
-                 device="cuda", seed=ransac.DEFAULT_SEED, fused=False, keypoints=None, overlap_ref=False):
+                 device="cuda", seed=ransac.DEFAULT_SEED, fused=False, keypoints=None, overlap_ref=False,
+                 gate_scorer=True):
         self.batch = int(batch)
+        # step_pipelined: the next step's scorer waits for this step's sweep
+        # (sfm_score_gate), so the side-stream sweep overlaps the solve only
+        self.gate_scorer = bool(gate_scorer)
         self.H, self.W = image_hw
         self.h, self.w = feat_hw
         self.C = int(channels)
@@ -140,6 +146,14 @@ class TwoViewHotPath:
             t.record_stream(side)       # allocator: live until the side stream is done with them
         with torch.cuda.stream(side):
             cost = self.sweep(ref_fea, tgt_fea, P, K, Kinv)
+        if self.gate_scorer:
+            # the next step's scorer waits for this sweep (sfm_score_gate): the
+            # sweep overlaps that step's solve, not its compute-bound scorer
+            ev = torch.cuda.Event()
+            ev.record(side)
+            self._gate_event = ev        # alive until the next RANSAC call has been issued
+            _lib.check(_lib.load().sfm_score_gate(ctypes.c_void_p(ev.cuda_event), _lib.stream_ptr(self.device)),
+                       "sfm_score_gate")
         return E, P, inl, cost
 
     def step_overlap(self, flow, K, ref_fea, tgt_fea):

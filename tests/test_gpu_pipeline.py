@@ -1,14 +1,17 @@
-"""The bench's default step order: TwoViewHotPath.step_pipelined runs each
-step's plane sweep on a side stream, overlapping the next step's pose stage.
-Steps issued back to back (so the overlap really happens) must give the same
-E, P, inlier counts and cost volume as plain sequential steps."""
+"""bench.py --pipeline: TwoViewHotPath.step_pipelined runs each step's plane
+sweep on a side stream, overlapping the next step's pose stage (and, with the
+score gate, not its scorer).  Steps issued back to back (so the overlap
+really happens) must give the same E, P, inlier counts and cost volume as
+plain sequential steps; the reference-half overlap and the score fence are
+tested below."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-def test_pipelined_steps_equal_plain_steps(cuda):
+@pytest.mark.parametrize("gate", [True, False])
+def test_pipelined_steps_equal_plain_steps(cuda, gate):
     from sfm_amd import synth
     from sfm_amd.pipeline import TwoViewHotPath
     B, C, L, fhw = 2, 32, 32, (94, 311)
@@ -17,7 +20,7 @@ def test_pipelined_steps_equal_plain_steps(cuda):
         flow, K, _, _ = synth.kitti_pair_batch(B, seed=s, device=cuda)
         ref, tgt = synth.features(B, C, *fhw, seed=s, device=cuda)
         steps.append((flow, K, ref, tgt))
-    mk = lambda: TwoViewHotPath(B, (376, 1242), fhw, C, L, 2, 1e-4, 1.0, True, 0.6, device=cuda)
+    mk = lambda: TwoViewHotPath(B, (376, 1242), fhw, C, L, 2, 1e-4, 1.0, True, 0.6, device=cuda, gate_scorer=gate)
     plain, piped = mk(), mk()
     outs = [piped.step_pipelined(*a) for a in steps]      # back to back: sweep i overlaps pose i+1
     torch.cuda.synchronize()
