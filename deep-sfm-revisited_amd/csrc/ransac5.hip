@@ -1749,20 +1749,21 @@ static int record_score_fence(hipStream_t s) {
   return SFM_OK;
 }
 
-// Score gate (sfm_score_gate): an event the next RANSAC call on a device
-// waits for right before its scoring phase (one-shot), so that a pipelined
-// caller can run the previous step's HBM-bound sweep beside this step's
-// latency-bound solve while keeping the compute-bound scorer to itself.
+// Score gate (sfm_score_gate): a library-owned event per device, recorded
+// on the caller's (side) stream; the next RANSAC call on that device waits for
+// it right before its scoring phase (one-shot), so that a pipelined caller can
+// run the previous step's HBM-bound sweep beside this step's latency-bound
+// solve while keeping the compute-bound scorer to itself.
 static hipEvent_t g_gate[kFenceDevices] = {};
+static bool g_gate_armed[kFenceDevices] = {};
 
 static int wait_score_gate(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_fence_mu);
   int dev = 0;
   if (int rc = stream_device(s, &dev)) return rc;
-  if (g_gate[dev]) {
-    const hipEvent_t ev = g_gate[dev];
-    g_gate[dev] = nullptr;
-    SFM_HIP(hipStreamWaitEvent(s, ev, 0));
+  if (g_gate_armed[dev]) {
+    g_gate_armed[dev] = false;
+    SFM_HIP(hipStreamWaitEvent(s, g_gate[dev], 0));
   }
   return SFM_OK;
 }
@@ -2002,11 +2003,24 @@ int sfm_score_fence_wait(void* stream) {
   return SFM_OK;
 }
 
-int sfm_score_gate(void* event, void* stream) {
+int sfm_score_gate(void* stream, int arm) {
   std::lock_guard<std::mutex> lk(g_fence_mu);
   int dev = 0;
   if (int rc = stream_device((hipStream_t)stream, &dev)) return rc;
-  g_gate[dev] = (hipEvent_t)event;
+  if (!arm) {
+    g_gate_armed[dev] = false;
+    return SFM_OK;
+  }
+  if (!g_gate[dev]) {
+    int cur = 0;
+    SFM_HIP(hipGetDevice(&cur));
+    SFM_HIP(hipSetDevice(dev));
+    const hipError_t e = hipEventCreateWithFlags(&g_gate[dev], hipEventDisableTiming);
+    SFM_HIP(hipSetDevice(cur));
+    SFM_HIP(e);
+  }
+  SFM_HIP(hipEventRecord(g_gate[dev], (hipStream_t)stream));
+  g_gate_armed[dev] = true;
   return SFM_OK;
 }
 

@@ -147,13 +147,10 @@ class TwoViewHotPath:
         with torch.cuda.stream(side):
             cost = self.sweep(ref_fea, tgt_fea, P, K, Kinv)
         if self.gate_scorer:
-            # the next step's scorer waits for this sweep (sfm_score_gate): the
-            # sweep overlaps that step's solve, not its compute-bound scorer
-            ev = torch.cuda.Event()
-            ev.record(side)
-            self._gate_event = ev        # alive until the next RANSAC call has been issued
-            _lib.check(_lib.load().sfm_score_gate(ctypes.c_void_p(ev.cuda_event), _lib.stream_ptr(self.device)),
-                       "sfm_score_gate")
+            # the next step's scorer waits for this sweep (sfm_score_gate, an
+            # event the library records on the side stream): the sweep overlaps
+            # that step's solve, not its compute-bound scorer
+            _lib.check(_lib.load().sfm_score_gate(ctypes.c_void_p(side.cuda_stream), 1), "sfm_score_gate")
         return E, P, inl, cost
 
     def step_overlap(self, flow, K, ref_fea, tgt_fea):

@@ -270,17 +270,17 @@ size_t sfm_plane_sweep_ref_planes_workspace_bytes(int batch, int channels, int h
 int sfm_score_fence_enable(int on);
 int sfm_score_fence_wait(void* stream);
 
-/* Score gate (round 5): the next RANSAC call (sfm_ransac5 / _packed / _flow)
- * whose stream is on the device of `stream` makes its stream wait for
- * `event` (a hipEvent_t) right before its scoring phase, and clears the gate
- * (one-shot; event NULL clears it).  A pipelined caller sets it to the event
- * recorded after the previous step's sweep on a side stream, so that sweep
- * overlaps this step's correspondence build and five-point solve but not the
- * scorer (sfm_amd.pipeline.TwoViewHotPath.step_pipelined).  The event must
- * stay valid until that RANSAC call has been issued.  No reference
+/* Score gate (round 5).  arm = 1: record the library's gate event (one per
+ * device) on `stream` and arm it: the next RANSAC call (sfm_ransac5 /
+ * _packed / _flow) whose stream is on that device makes its stream wait for
+ * the event right before its scoring phase, and disarms the gate (one-shot).
+ * arm = 0 disarms it.  A pipelined caller arms it on the side stream right
+ * after the previous step's sweep, so that sweep overlaps this step's
+ * correspondence build and five-point solve but not the scorer
+ * (sfm_amd.pipeline.TwoViewHotPath.step_pipelined).  No reference
  * counterpart: the reference's steps are serial (essential_matrix.cu:190-280
  * then PSNet.py:130-158). */
-int sfm_score_gate(void* event, void* stream);
+int sfm_score_gate(void* stream, int arm);
 int sfm_plane_sweep_ref_planes(const float* ref, int batch, int channels, int h, int w, int nlabel, int out_dtype,
                                void* cost, void* workspace, size_t workspace_bytes, void* stream);
 int sfm_plane_sweep_psnet_warped_half(const float* ref, const float* tgt, int batch, int channels, int h, int w,
