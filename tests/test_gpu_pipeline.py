@@ -118,3 +118,43 @@ def test_overlap_hot_path_on_non_current_device():
         c1 = plain.step(flow, K, ref, tgt)[3]
         torch.cuda.synchronize(dev)
     assert torch.equal(c1, c2)
+
+
+def test_score_gate_one_shot(cuda):
+    """sfm_score_gate(stream, 1) records the library's gate event on a side
+    stream and arms it: the next RANSAC call on the device holds its scoring
+    phase until the side stream reaches that point, and disarms the gate; the
+    call after it does not wait; arm = 0 disarms without waiting."""
+    import ctypes
+    from sfm_amd import _lib, synth
+    lib = _lib.load()
+    B = 2
+    flow, K, _, _ = synth.kitti_pair_batch(B, seed=5, device=cuda)
+    from sfm_amd.pipeline import TwoViewHotPath
+    hp = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 8, device=cuda)
+    Kinv = hp.k_inverse(K)
+    hp.pose(flow, K, Kinv)                                   # warm: kernels loaded, buffers touched
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(device=cuda)
+    main = torch.cuda.current_stream(cuda)
+
+    def timed_pose(sleep_cycles, arm):
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(sleep_cycles)
+        if arm is not None:
+            assert lib.sfm_score_gate(ctypes.c_void_p(side.cuda_stream), arm) == 0
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record(main)
+        hp.pose(flow, K, Kinv)
+        t1.record(main)
+        torch.cuda.synchronize()
+        return t0.elapsed_time(t1)
+
+    base = timed_pose(1000, None)                            # no gate: the pose stage alone
+    sleep = 200_000_000                                      # ~0.1 s on the side stream
+    gated = timed_pose(sleep, 1)
+    assert gated > base + 20.0, (base, gated)                # held for the side stream
+    free = timed_pose(sleep, None)                           # the gate was consumed
+    assert free < base + 20.0, (base, free)
+    disarmed = timed_pose(sleep, 0)                          # arm = 0: nothing to wait for
+    assert disarmed < base + 20.0, (base, disarmed)
