@@ -40,7 +40,7 @@ struct Tuning {
   int score_mf_prune = 880;      // k_score_mf2 count-bound pruning: the first launch's share of each pair's
                                  // spans in per mille (0: off; one launch); later pruning points per pair from
                                  // k_mf2_split (an empty middle launch when the pair's own point is not later)
-  int score_mf_prune_margin = 25; // the pruning point: 1 - (inlier ratio) + margin, per mille (k_mf2_split)
+  int score_mf_prune_margin = 10; // the pruning point: 1 - (inlier ratio) + margin, per mille (k_mf2_split)
   int score_mf_chunk = 64;       // k_score_mf2: smallest unit range a block claims (32-candidate tiles of a span);
                                  // 64 measured ~1 % faster than 128 with pruning (profiles/r05_prune_ab.txt)
   int score_mf_blocks_per_cu = 1; // k_score_mf persistent grid (LDS: one block per CU)

@@ -473,7 +473,7 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     Winner, count, E, P unchanged; only with
  *                                     num_test == num_ransac_test, no per-
  *                                     hypothesis scores, >= 32 spans per pair
- *     "score_mf_prune_margin" 0..200  that margin, per mille (25)
+ *     "score_mf_prune_margin" 0..200  that margin, per mille (10)
  *     "roots_split"           0, 1, 2 k_roots_split: falsi nodes shared by the wave's
  *                                     64 lanes (1, default), or by the four waves of
  *                                     a block (2, measured 2-6 % slower), speculated
