@@ -213,3 +213,34 @@ def test_pipeline_and_overlap_ref_are_exclusive():
     with pytest.raises(SystemExit):
         bench.parse(["--pipeline", "--overlap-ref", "score"])
     assert bench.parse(["--overlap-ref", "score"]).overlap_ref == "score"
+
+
+def test_pmc_summary_sums_template_instances(tmp_path):
+    """scripts/pmc_summary.py: a path key's per-step figure sums every
+    dispatch of its kernels per step, and launches of template instances of
+    one kernel (k_score_mf2<Src, false> and <Src, true>) add up in
+    launches_sampled (round 5: the pruned scorer's three launches)."""
+    import csv
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("pmc_summary", os.path.join(ROOT, "scripts", "pmc_summary.py"))
+    ps = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ps)
+    src = tmp_path / "pmc"
+    (src / "p1").mkdir(parents=True)
+    a = "_ZN3sfm11k_score_mf2INS_9PackedSrcELb0EEEvT_NS_10PairParamsE"
+    c = "_ZN3sfm11k_score_mf2INS_9PackedSrcELb1EEEvT_NS_10PairParamsE"
+    m = "_ZN3sfm10k_mf_candsEiPKiPKdPDF16_NS_8MfParamsEPyPi"
+    rows = []
+    for step in range(2):                          # per step: cands, A, B (false), C (true)
+        base = 10 * step
+        rows += [(m, base + 1, 10.0), (a, base + 2, 100.0), (a, base + 3, 1.0), (c, base + 4, 5.0)]
+    with open(src / "p1" / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Dispatch_Id", "Counter_Name", "Counter_Value"])
+        for name, d, v in rows:
+            w.writerow([name, d, "SQ_WAVES", v])
+    dst = tmp_path / "out.json"
+    ps.main(str(src), str(dst), "c2")
+    k = json.load(open(dst))["kernels"]["ransac_score"]
+    assert k["launches_sampled"] == {"k_mf_cands": 2, "k_score_mf2": 6}
+    assert abs(k["SQ_WAVES"] - 116.0) < 1e-9               # 10 + 100 + 1 + 5 per step
