@@ -32,6 +32,10 @@ def test_ransac_golden(golden, cuda, case):
     g = golden("ransac.npz")[case]
     n, nt, nr, it, thr, cheir, seed = g["params"]
     r = _ransac_gpu(g["q"], g["qp"], int(nt), int(nr), int(it), float(thr), bool(cheir), cuda, int(seed))
+    from sfm_amd import _lib
+    # per-hypothesis scores requested: no pruning; num_test != num_ransac_test
+    # (two count arrays) takes the item-major k_score_mf
+    assert _lib.last_scorer() == ("k_score_mf2" if int(nt) == int(nr) else "k_score_mf"), _lib.last_scorer()
     assert r["winner"] == int(g["winner"])
     assert r["inliers"] == int(g["inliers"])
     assert np.array_equal(r["scores"], g["hyp_score"])
