@@ -29,6 +29,14 @@ def test_header_symbols_exported():
     assert lib.sfm_abi_version() == 1
 
 
+def test_integration_indexes_every_entry_point():
+    """INTEGRATION.md's entry-point index names every declared function (the
+    bindings a maintainer writes against the reference's interface)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    missing = [n for n in _declared() if f"`{n}`" not in doc]
+    assert not missing, missing
+
+
 def test_workspace_query():
     from sfm_amd import _lib
     lib = _lib.load()
