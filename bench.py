@@ -17,6 +17,8 @@ pose stage); the timed region ends after the last sweep either way.
   c4      8 indoor 640x480 pairs, N=285,200, H=2048, L=64 (configs[3])
   sparse  c2 with the SIFT-keypoint branch of pose_by_ransac: N=2,048
           keypoints per pair (SFMnet.py:250-254); the solve dominates
+  c5      c2 with H=8192 hypotheses (ransac_iter 16; LO-RANSAC's count,
+          configs[4]; its IRLS refinement is not in the step)
 
 Multi-GPU: one process per GPU.  Under torchrun the ranks come from its env;
 ``python bench.py --gpus N`` with no WORLD_SIZE starts the N ranks itself
@@ -60,6 +62,7 @@ CONFIGS = {
     "c3": (4, "kitti", 8, 128, "bf16", 0),
     "c4": (8, "indoor", 4, 64, "fp32", 0),
     "sparse": (8, "kitti", 8, 128, "fp32", 2048),
+    "c5": (8, "kitti", 16, 128, "fp32", 0),      # H = 8192 hypotheses (LO-RANSAC's count; its IRLS is not timed)
 }
 
 

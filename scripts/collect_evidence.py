@@ -37,7 +37,7 @@ def json_line(log):
 
 def main(R):
     done = []
-    for cfg in ("c2", "sparse", "c3", "c4"):
+    for cfg in ("c2", "sparse", "c3", "c4", "c5"):
         log = os.path.join(OUT, f"{R}_bench_{cfg}.log")
         if os.path.exists(log) and json_line(log):
             p = next_path(f"{R}_bench_{cfg}", ".json")

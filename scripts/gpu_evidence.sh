@@ -37,7 +37,7 @@ if [ "${SKIP_PMC:-0}" != "1" ]; then
       || { tail -20 gpurun_out/${R}_pmc_c3.log; exit 1; }
 fi
 if [ "${SKIP_CONFIGS:-0}" != "1" ]; then
-  for cfg in sparse c3 c4; do
+  for cfg in sparse c3 c4 c5; do
     timeout -k 10 300 python -u bench.py --config $cfg --steps 20 --warmup 3 --no-cpu-baseline --no-regularize \
         > gpurun_out/${R}_bench_$cfg.log 2>&1 || { tail -20 gpurun_out/${R}_bench_$cfg.log; exit 1; }
     grep '^{' gpurun_out/${R}_bench_$cfg.log | cut -c1-300

@@ -46,7 +46,7 @@ def kernel_key(name):
 
 # bench.py CONFIGS: (pairs per GPU, scene, iters, nlabel, cost dtype, keypoints)
 WORKLOADS = {"c2": (8, 8, 128, "fp32"), "c3": (4, 8, 128, "bf16"), "c4": (8, 4, 64, "fp32"),
-             "sparse": (8, 8, 128, "fp32")}
+             "sparse": (8, 8, 128, "fp32"), "c5": (8, 16, 128, "fp32")}
 
 
 def main(src, dst, config="c2"):
