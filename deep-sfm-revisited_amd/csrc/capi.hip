@@ -112,7 +112,6 @@ const TuneKey kTuneKeys[] = {
     {"sweep_flat", &sfm::Tuning::sweep_flat, [](int v) { return v >= 0 && v <= 3; }},
     {"sweep_buffer", &sfm::Tuning::sweep_buffer, v_01},
     {"sweep_share", &sfm::Tuning::sweep_share, v_01},
-    {"sweep_ref16", &sfm::Tuning::sweep_ref16, v_01},
     {"sweep_store_wt", &sfm::Tuning::sweep_store_wt, [](int v) { return v >= -1 && v <= 3; }},
     {"sweep_store_nt", &sfm::Tuning::sweep_store_nt, [](int v) { return v >= 0 && v <= 2; }},
     {"sweep_store_px", &sfm::Tuning::sweep_store_px, [](int v) { return v >= -1 && v <= 8 && (v <= 2 || v == 4 || v == 8); }},

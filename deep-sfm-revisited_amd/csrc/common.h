@@ -24,8 +24,6 @@ struct Tuning {
   int sweep_share = 0;           // k_sweep_tile fast path: right-hand taps from the next lane's left-hand taps (DPP)
   int sweep_store_wt = -1;       // 16-byte sweep stores' cache policy: 0 by sweep_store_nt, 1 sc1, 2 sc0 sc1, 3 nt sc1;
                                  // -1 (default): fp32 volumes 3, bf16 by sweep_store_nt
-  int sweep_ref16 = 0;           // bf16 wide stores: reference rows copied from a bf16 copy made by k_tgt_quads (1;
-                                 // measured 1 % slower on c3, profiles/r05_sweep_store_wt.txt), or converted per plane (0)
   int sweep_store_px = -1;       // k_sweep_tile fast path: 16-byte lane stores via LDS, 1/2/4/8 pixels per lane; 0: plain; -1: bf16 2, fp32 1
   int sweep_store_nt = 2;        // k_sweep_tile fast path: volume stores with sc0 nt (streaming); 2: bf16 volumes and
                                  // fp32 volumes of slabs <= 6 MiB (measured by shape)

@@ -1749,22 +1749,34 @@ static int record_score_fence(hipStream_t s) {
   return SFM_OK;
 }
 
-// Score gate (sfm_score_gate): a library-owned event per device, recorded
-// on the caller's (side) stream; the next RANSAC call on that device waits for
-// it right before its scoring phase (one-shot), so that a pipelined caller can
-// run the previous step's HBM-bound sweep beside this step's latency-bound
-// solve while keeping the compute-bound scorer to itself.
-static hipEvent_t g_gate[kFenceDevices] = {};
-static bool g_gate_armed[kFenceDevices] = {};
+// Score gate (sfm_score_gate): a library-owned event per (device, waiting
+// stream), recorded on the caller's (side) stream; the next RANSAC call issued
+// on that waiting stream waits for it right before its scoring phase
+// (one-shot), so that a pipelined caller can run the previous step's
+// HBM-bound sweep beside this step's latency-bound solve while keeping the
+// compute-bound scorer to itself.  RANSAC calls on any other stream -- another
+// hot path on the same device, a plain computeP -- neither wait for nor
+// consume it.
+constexpr int kGates = 32;
+struct ScoreGate {
+  int dev = -1;                  // -1: free slot
+  hipStream_t waiter = nullptr;  // the stream whose next scoring phase waits
+  hipEvent_t ev = nullptr;       // kept when the slot is freed (reused on evdev)
+  int evdev = -1;                // the device ev was created on
+  bool armed = false;
+};
+static ScoreGate g_gates[kGates];
 
 static int wait_score_gate(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_fence_mu);
   int dev = 0;
   if (int rc = stream_device(s, &dev)) return rc;
-  if (g_gate_armed[dev]) {
-    g_gate_armed[dev] = false;
-    SFM_HIP(hipStreamWaitEvent(s, g_gate[dev], 0));
-  }
+  for (ScoreGate& g : g_gates)
+    if (g.armed && g.dev == dev && g.waiter == s) {
+      g.armed = false;
+      g.dev = -1;
+      SFM_HIP(hipStreamWaitEvent(s, g.ev, 0));
+    }
   return SFM_OK;
 }
 
@@ -2003,24 +2015,44 @@ int sfm_score_fence_wait(void* stream) {
   return SFM_OK;
 }
 
-int sfm_score_gate(void* stream, int arm) {
+int sfm_score_gate(void* stream, void* waiter, int arm) {
   std::lock_guard<std::mutex> lk(g_fence_mu);
   int dev = 0;
   if (int rc = stream_device((hipStream_t)stream, &dev)) return rc;
+  ScoreGate* slot = nullptr;
+  for (ScoreGate& g : g_gates)
+    if (g.dev == dev && g.waiter == (hipStream_t)waiter) slot = &g;
   if (!arm) {
-    g_gate_armed[dev] = false;
+    if (slot) {
+      slot->armed = false;
+      slot->dev = -1;
+    }
     return SFM_OK;
   }
-  if (!g_gate[dev]) {
+  if (!slot) {
+    for (ScoreGate& g : g_gates)                             // a free slot, one with this device's event first
+      if (g.dev < 0 && (!slot || (g.evdev == dev && slot->evdev != dev))) slot = &g;
+    SFM_REQUIRE(slot != nullptr, "score gate: too many armed (device, stream) gates");
+  }
+  if (slot->evdev != dev) {
+    if (slot->ev) {                                          // an event of another device
+      hipEvent_t old = slot->ev;
+      slot->ev = nullptr;
+      slot->evdev = -1;
+      SFM_HIP(hipEventDestroy(old));
+    }
     int cur = 0;
     SFM_HIP(hipGetDevice(&cur));
     SFM_HIP(hipSetDevice(dev));
-    const hipError_t e = hipEventCreateWithFlags(&g_gate[dev], hipEventDisableTiming);
+    const hipError_t e = hipEventCreateWithFlags(&slot->ev, hipEventDisableTiming);
     SFM_HIP(hipSetDevice(cur));
     SFM_HIP(e);
+    slot->evdev = dev;
   }
-  SFM_HIP(hipEventRecord(g_gate[dev], (hipStream_t)stream));
-  g_gate_armed[dev] = true;
+  SFM_HIP(hipEventRecord(slot->ev, (hipStream_t)stream));
+  slot->dev = dev;
+  slot->waiter = (hipStream_t)waiter;
+  slot->armed = true;
   return SFM_OK;
 }
 

@@ -614,9 +614,12 @@ __device__ __forceinline__ int swz4(int chunk, int p) { return chunk ^ ((p >> 2)
 __global__ __launch_bounds__(kConvThreads, 2) void k_conv3_f32(
     const float* __restrict__ in, int cin, const float* __restrict__ wpk, const float* __restrict__ scale,
     const float* __restrict__ bias, const float* __restrict__ res, int relu, float* __restrict__ out,
-    float* __restrict__ out1, int D, int H, int W, int ntx, int nty, int nblk, int per_xcd) {
+    float* __restrict__ out1, int D, int H, int W, int ntx, int nty, int nblk, int per_xcd,
+    const int* __restrict__ only_if) {
   __shared__ __attribute__((aligned(16))) unsigned char lds_in[kF32InBytes];
   __shared__ __attribute__((aligned(16))) unsigned char lds_w[kF32WBytes];
+  // the fp32x3 layer's out-of-range re-run: nothing to do unless its flag is set
+  if (only_if && *only_if == 0) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int logical = (int)(blockIdx.x % kXcds) * per_xcd + (int)(blockIdx.x / kXcds);   // XCD-aware, d-fastest
@@ -743,6 +746,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void k_conv3_f32(
 // k_conv3) and are split on their way into LDS (one float4 -> 8 B hi + 8 B lo).
 // ---------------------------------------------------------------------------
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr float kF16Max = 65504.0f;                          // the largest finite f16
 
 __device__ __forceinline__ void split_f16x4(const float4 v, uint2& hi, uint2& lo) {
   const f16x4 h = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
@@ -755,7 +759,8 @@ __device__ __forceinline__ void split_f16x4(const float4 v, uint2& hi, uint2& lo
 __global__ __launch_bounds__(kConvThreads, 2) void k_conv3_x3(
     const float* __restrict__ in, int cin, const float* __restrict__ wpk, int wexp, const float* __restrict__ scale,
     const float* __restrict__ bias, const float* __restrict__ res, int relu, float* __restrict__ out,
-    float* __restrict__ out1, int D, int H, int W, int ntx, int nty, int nblk, int per_xcd) {
+    float* __restrict__ out1, int D, int H, int W, int ntx, int nty, int nblk, int per_xcd,
+    int* __restrict__ range_flag) {
   __shared__ __attribute__((aligned(16))) unsigned char lds_in[kF32InBytes];
   __shared__ __attribute__((aligned(16))) unsigned char lds_w[kF32WBytes];
   const int tid = threadIdx.x;
@@ -821,10 +826,22 @@ __global__ __launch_bounds__(kConvThreads, 2) void k_conv3_x3(
     *reinterpret_cast<uint2*>(row + (mc & 1) * 8 + swz4(mc >> 1, sw) * 16) = hi;
     *reinterpret_cast<uint2*>(row + (mc & 1) * 8 + swz4(2 + (mc >> 1), sw) * 16) = lo;
   };
+  // the largest staged activation magnitude: past the f16 maximum x_hi would
+  // be infinite (NaNs drop out of fmaxf, and propagate alike on both paths)
+  float amax = 0.0f;
+  auto track = [&](const float4 v) {
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  };
   auto commit = [&]() {
 #pragma unroll
-    for (int ry = 0; ry < kHaloY; ++ry) put(lds_in + (ry * kHaloX + mpx) * kF32Pix, mpx, pin[ry]);
-    if (hasx) put(lds_in + (ery * kHaloX + epx) * kF32Pix, epx, pin[kHaloY]);
+    for (int ry = 0; ry < kHaloY; ++ry) {
+      track(pin[ry]);
+      put(lds_in + (ry * kHaloX + mpx) * kF32Pix, mpx, pin[ry]);
+    }
+    if (hasx) {
+      track(pin[kHaloY]);
+      put(lds_in + (ery * kHaloX + epx) * kF32Pix, epx, pin[kHaloY]);
+    }
 #pragma unroll
     for (int k = 0; k < 5; ++k)
       if (wt0 + 2 * k < 9) {
@@ -873,6 +890,9 @@ __global__ __launch_bounds__(kConvThreads, 2) void k_conv3_x3(
     }
   }
 
+  // an activation outside the f16 range: flag the layer for its fp32 re-run
+  // (sfm_conv3_f32x3 with a range flag; a plain vector store, idempotent)
+  if (range_flag && amax > kF16Max) *range_flag = 1;
   // epilogue: k_conv3_f32's, with the weights' 2^wexp folded into the scale
   // (exact: a power of two)
   const float unscale = __builtin_ldexpf(1.0f, -wexp);
@@ -1080,14 +1100,14 @@ int sfm_conv3_f32(const float* in, int batch, int cin, int depth, int h, int w, 
   const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
   hipLaunchKernelGGL(k_conv3_f32, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, in, cin, weights,
                      scale, bias, residual, relu, cout == 32 ? out : nullptr, cout == 1 ? out : nullptr, depth, h, w,
-                     ntx, nty, (int)nblk, per_xcd);
+                     ntx, nty, (int)nblk, per_xcd, (const int*)nullptr);
   SFM_LAUNCHED();
   return SFM_OK;
 }
 
 int sfm_conv3_f32x3(const float* in, int batch, int cin, int depth, int h, int w, const float* weights, int wexp,
                     const float* scale, const float* bias, const float* residual, int relu, int cout, float* out,
-                    void* stream) {
+                    int* range_flag, void* stream) {
   SFM_REQUIRE(in && weights && scale && bias && out, "null pointer argument");
   SFM_REQUIRE(cin == 32 || cin == 64, "cin must be 32 or 64");
   SFM_REQUIRE(cout == 32 || cout == 1, "cout must be 32 or 1");
@@ -1105,10 +1125,21 @@ int sfm_conv3_f32x3(const float* in, int batch, int cin, int depth, int h, int w
   const int64_t nblk = (int64_t)ntx * nty * batch * depth;
   SFM_REQUIRE(nblk < ((int64_t)1 << 31) - 8, "conv grid too large");
   const int per_xcd = (int)((nblk + kXcds - 1) / kXcds);
+  SFM_REQUIRE(range_flag == nullptr || ((uintptr_t)range_flag & 3) == 0, "range_flag must be 4-byte aligned");
+  if (range_flag) SFM_HIP(hipMemsetAsync(range_flag, 0, sizeof(int), s));
   hipLaunchKernelGGL(k_conv3_x3, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, in, cin, weights, wexp,
                      scale, bias, residual, relu, cout == 32 ? out : nullptr, cout == 1 ? out : nullptr, depth, h, w,
-                     ntx, nty, (int)nblk, per_xcd);
+                     ntx, nty, (int)nblk, per_xcd, range_flag);
   SFM_LAUNCHED();
+  if (range_flag) {
+    // stream-ordered fallback: the same layer on the f32 matrix cores (the
+    // same weights: k_conv3_x3 applies 2^wexp itself) re-writes out, its
+    // blocks returning at once unless an activation left the f16 range
+    hipLaunchKernelGGL(k_conv3_f32, dim3((unsigned)(per_xcd * kXcds)), dim3(kConvThreads), 0, s, in, cin, weights,
+                       scale, bias, residual, relu, cout == 32 ? out : nullptr, cout == 1 ? out : nullptr, depth, h,
+                       w, ntx, nty, (int)nblk, per_xcd, (const int*)range_flag);
+    SFM_LAUNCHED();
+  }
   return SFM_OK;
 }
 

@@ -93,8 +93,7 @@ __device__ __forceinline__ void psnet_prep_pair(const PsnetPrep& q, int B, int b
 __global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4, int hw, f32x4* __restrict__ tq,
                             const float* __restrict__ pose, const float* __restrict__ K4,
                             const float* __restrict__ K4inv, Proj* __restrict__ projs, int L, float dmax,
-                            float dstep, float* __restrict__ depths, PsnetPrep prep,
-                            const float* __restrict__ ref = nullptr, unsigned short* __restrict__ ref16 = nullptr) {
+                            float dstep, float* __restrict__ depths, PsnetPrep prep) {
   // grid (pixels, quads, pairs): no integer division per thread; the uniform
   // per-pair and per-plane tables from the first quad row of pair 0
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -123,15 +122,6 @@ __global__ void k_tgt_quads(const float* __restrict__ tgt, int B, int C, int C4,
     v[k] = c < C ? tgt[((size_t)b * C + c) * hw + i] : 0.0f;
   }
   tq[((size_t)b * C4 + q) * hw + i] = v;
-  if (ref16) {
-    // a bf16 volume's reference rows, converted once (k_sweep_tile's 16-byte
-    // stores copy them from here instead of converting per plane)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = 4 * q + k;
-      if (c < C) ref16[((size_t)b * C + c) * hw + i] = to_bf16(ref[((size_t)b * C + c) * hw + i]);
-    }
-  }
 }
 
 static dim3 quads_grid(int B, int C4, int hw, int extra) {
@@ -401,7 +391,6 @@ struct FlatGeom {
   float inv_w;
   float dmax, dstep;
   const float* depths;   // plane depths (k_tgt_quads), or null
-  const unsigned short* ref16;   // bf16 volumes: the reference rows in bf16 [B][C][hw] (k_tgt_quads), or null
   int wpol;        // 16-byte stores' cache policy when not -1 (16 sc1, 17 sc0 sc1, 18 nt sc1; sweep_store_wt)
 };
 
@@ -834,10 +823,8 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
           __builtin_amdgcn_raw_buffer_load_b32(rref, (unsigned)ps[j] * 4u, (unsigned)c * g.hw * 4u, 0));
   };
   constexpr bool LATE = WIDE && NJ == 8;        // registers: the reference rows at their stores
-  // bf16 wide stores with the converted reference rows: copied at their stores
-  const bool r16 = WIDE && BF && g.ref16 != nullptr;
   float cp[LATE ? 1 : G][NJ];
-  if (!LATE && !r16 && g.ref_rows && g.write_ref) {
+  if (!LATE && g.ref_rows && g.write_ref) {
 #pragma unroll
     for (int c = 0; c < G; ++c) load_ref_row(c, cp[LATE ? 0 : c]);
   }
@@ -1017,34 +1004,7 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
       }
       flush((unsigned)(g.ref_rows + c0 + c));
     }
-    if (g.ref_rows && g.write_ref && r16) {
-      // the reference rows straight from their bf16 copy: lane (rr, cl)
-      // loads the EPL pixels it stores (plane l0's or, past its end, the next
-      // plane's pixel offsets; a chunk across the plane boundary by element)
-      const __amdgpu_buffer_rsrc_t r16r =
-          buf_rsrc(g.ref16 + ((size_t)b * g.C + c0) * g.hw, (unsigned)G * g.hw * 2u);
-      int p0 = woff + EPL * cl - l0 * g.hw;
-      while (p0 >= g.hw) p0 -= g.hw;
-      const bool wrap = p0 + EPL > g.hw;
-#pragma unroll
-      for (int c = 0; c < G; c += RPS) {
-        const unsigned so = (unsigned)(c + rr) * g.hw * 2u;
-        u32x4 x;
-        if (!wrap) {
-          x = __builtin_amdgcn_raw_buffer_load_b128(r16r, (unsigned)p0 * 2u, so, 0);
-        } else {
-          unsigned hv[EPL];
-#pragma unroll
-          for (int e = 0; e < EPL; ++e) {
-            const int pe = p0 + e < g.hw ? p0 + e : p0 + e - g.hw;
-            hv[e] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(r16r, (unsigned)pe * 2u, so, 0);
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) x[e] = hv[2 * e] | (hv[2 * e + 1] << 16);
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(x, rout, voff + (unsigned)(c0 + c) * row_bytes, 0, POL);
-      }
-    } else if (g.ref_rows && g.write_ref) {
+    if (g.ref_rows && g.write_ref) {
 #pragma unroll
       for (int c = 0; c < G; c += RPS) {
 #pragma unroll
@@ -1465,13 +1425,8 @@ static size_t sweep_proj_bytes(int B) { return ((size_t)B * sizeof(Proj) + 255) 
 // sfm_plane_sweep_psnet: float32 pose, K4, K4inv per pair (12 + 9 + 9 floats)
 static size_t sweep_psnet_bytes(int B) { return ((size_t)B * 30 * sizeof(float) + 255) & ~(size_t)255; }
 // what launch_sweep uses: quads, Proj table, plane depths
-// the bf16 copy of the reference rows (bf16 volumes with even h*w)
-static size_t sweep_ref16_bytes(int B, int C, int h, int w) {
-  return ((size_t)B * C * (size_t)h * w * sizeof(unsigned short) + 255) & ~(size_t)255;
-}
 static size_t sweep_core_bytes(int B, int C, int h, int w) {
-  return sweep_quads_bytes(B, C, h, w) + sweep_proj_bytes(B) + kDepthTable * sizeof(float) +
-         sweep_ref16_bytes(B, C, h, w);
+  return sweep_quads_bytes(B, C, h, w) + sweep_proj_bytes(B) + kDepthTable * sizeof(float);
 }
 // the public size: the core plus the sfm_plane_sweep_psnet operands at its end
 static size_t sweep_ws_bytes(int B, int C, int h, int w) { return sweep_core_bytes(B, C, h, w) + sweep_psnet_bytes(B); }
@@ -1513,15 +1468,10 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
   f32x4* tq = (f32x4*)ws;
   Proj* projs = reinterpret_cast<Proj*>((char*)ws + sweep_quads_bytes(B, C, h, w));
   float* depths = L <= kDepthTable ? reinterpret_cast<float*>((char*)projs + sweep_proj_bytes(B)) : nullptr;
-  // bf16 volume with its reference rows and an even h*w (every plane's copy
-  // then starts 4-byte aligned): the rows are converted once here
-  unsigned short* ref16 = nullptr;
-  if (out_dtype == 1 && with_ref && write_ref && hw % 2 == 0 && tuning().sweep_ref16)
-    ref16 = reinterpret_cast<unsigned short*>((char*)projs + sweep_proj_bytes(B) + kDepthTable * sizeof(float));
   {
     ProfScope ps("sweep_tgt_quads", s);
     hipLaunchKernelGGL(k_tgt_quads, quads_grid(B, g.C4, hw, std::max(B, L)), dim3(256), 0, s, tgt, B, C, g.C4, hw, tq,
-                       pose, K4, K4inv, projs, L, g.dmax, g.dstep, depths, prep, ref, ref16);
+                       pose, K4, K4inv, projs, L, g.dmax, g.dstep, depths, prep);
   }
   SFM_LAUNCHED();
   const char* pname = with_ref ? "plane_sweep" : "plane_sweep_warped";
@@ -1623,7 +1573,6 @@ static int launch_sweep(bool with_ref, const float* ref, const float* tgt, int B
     fg.inv_w = 1.0f / (float)w;
     fg.dmax = g.dmax; fg.dstep = g.dstep;
     fg.depths = depths;
-    fg.ref16 = (mode == 2 && store_px) ? ref16 : nullptr;
     {
       // auto (-1): fp32 volumes nt sc1 (write-through: the volume's lines do
       // not stay in the XCD's L2, where plain / nt stores keep them), bf16 by

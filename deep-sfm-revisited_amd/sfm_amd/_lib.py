@@ -52,7 +52,7 @@ _SIGS = [
       _c_dp]),
     ("sfm_score_fence_enable", ctypes.c_int, [ctypes.c_int]),
     ("sfm_score_fence_wait", ctypes.c_int, [_c_dp]),
-    ("sfm_score_gate", ctypes.c_int, [_c_dp, ctypes.c_int]),
+    ("sfm_score_gate", ctypes.c_int, [_c_dp, _c_dp, ctypes.c_int]),
     ("sfm_plane_sweep_ref_planes_workspace_bytes", ctypes.c_size_t,
      [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("sfm_plane_sweep_ref_planes", ctypes.c_int,
@@ -102,7 +102,7 @@ _SIGS = [
       ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
     ("sfm_conv3_f32x3", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp, ctypes.c_int, _c_dp, _c_dp,
-      _c_dp, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
+      _c_dp, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp, _c_dp]),
     ("sfm_to_channels_last_f32", ctypes.c_int,
      [_c_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp]),
     ("sfm_score_essentials_workspace_bytes", ctypes.c_size_t, [ctypes.c_int, ctypes.c_int]),

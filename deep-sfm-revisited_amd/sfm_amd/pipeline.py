@@ -148,9 +148,11 @@ class TwoViewHotPath:
             cost = self.sweep(ref_fea, tgt_fea, P, K, Kinv)
         if self.gate_scorer:
             # the next step's scorer waits for this sweep (sfm_score_gate, an
-            # event the library records on the side stream): the sweep overlaps
-            # that step's solve, not its compute-bound scorer
-            _lib.check(_lib.load().sfm_score_gate(ctypes.c_void_p(side.cuda_stream), 1), "sfm_score_gate")
+            # event the library records on the side stream, armed for this
+            # hot path's main stream only): the sweep overlaps that step's
+            # solve, not its compute-bound scorer
+            _lib.check(_lib.load().sfm_score_gate(ctypes.c_void_p(side.cuda_stream),
+                                                  ctypes.c_void_p(main.cuda_stream), 1), "sfm_score_gate")
         return E, P, inl, cost
 
     def step_overlap(self, flow, K, ref_fea, tgt_fea):

@@ -184,7 +184,9 @@ class CostRegularization(nn.Module):
         ``precision``: "fp32x3" (default: the reference's fp32 activations
         and weights, each product formed from a two-term f16 split of both
         operands on the f16 matrix cores, sfm_conv3_f32x3: ~2^-21 per product,
-        within the float64 depth bars at 3x the speed of "fp32"), "fp32"
+        within the float64 depth bars at 3x the speed of "fp32"; a layer whose
+        input holds an activation beyond the f16 maximum 65504 is re-run as
+        "fp32" on the device, see sfm_hip.h), "fp32"
         (fp32 operands on the f32 matrix cores, sfm_conv3_f32: float32
         arithmetic exactly, in another summation order),
         "fp16" (fp16
@@ -221,6 +223,9 @@ class CostRegularization(nn.Module):
                              stream), "sfm_to_channels_last")
             bufs = [torch.empty((B, L, h, w, 32), dtype=adt, device=dev) for _ in range(3)]
             out = torch.empty((B, 1, L, h, w), dtype=torch.float32, device=dev)
+            # fp32x3: one range flag per layer -- a layer whose input leaves the
+            # f16 range is re-run by sfm_conv3_f32 inside the same call, stream-ordered
+            flags = torch.empty(len(packed), dtype=torch.int32, device=dev) if precision == "fp32x3" else None
             cur, keep = x, None           # keep: the block input of a residual pair (cost0)
             for li, lay in enumerate(packed):
                 if lay["cout"] == 1:
@@ -231,7 +236,7 @@ class CostRegularization(nn.Module):
                 if precision == "fp32x3":
                     rc = x3(_lib.ptr(cur), B, lay["cin"], L, h, w, _lib.ptr(lay["w"]), lay["wexp"],
                             _lib.ptr(lay["scale"]), _lib.ptr(lay["bias"]), None if res is None else _lib.ptr(res),
-                            1 if lay["relu"] else 0, lay["cout"], _lib.ptr(dst), stream)
+                            1 if lay["relu"] else 0, lay["cout"], _lib.ptr(dst), flags[li].data_ptr(), stream)
                 else:
                     rc = conv(_lib.ptr(cur), B, lay["cin"], L, h, w, _lib.ptr(lay["w"]), _lib.ptr(lay["scale"]),
                               _lib.ptr(lay["bias"]), None if res is None else _lib.ptr(res), 1 if lay["relu"] else 0,

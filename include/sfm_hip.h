@@ -270,17 +270,22 @@ size_t sfm_plane_sweep_ref_planes_workspace_bytes(int batch, int channels, int h
 int sfm_score_fence_enable(int on);
 int sfm_score_fence_wait(void* stream);
 
-/* Score gate (round 5).  arm = 1: record the library's gate event (one per
- * device) on `stream` and arm it: the next RANSAC call (sfm_ransac5 /
- * _packed / _flow) whose stream is on that device makes its stream wait for
- * the event right before its scoring phase, and disarms the gate (one-shot).
- * arm = 0 disarms it.  A pipelined caller arms it on the side stream right
- * after the previous step's sweep, so that sweep overlaps this step's
- * correspondence build and five-point solve but not the scorer
+/* Score gate (round 5; scoped to a waiting stream in round 6).  arm = 1:
+ * record a library-owned event on `stream` and arm it for `waiter`: the next
+ * RANSAC call (sfm_ransac5 / _packed / _flow) issued on the stream `waiter`
+ * (on stream's device) makes `waiter` wait for the event right before its
+ * scoring phase, and disarms the gate (one-shot).  RANSAC calls on any other
+ * stream neither wait for nor consume it, so a second hot path or a plain
+ * computeP on the same device is unaffected.  Re-arming for the same waiter
+ * replaces the previous gate; arm = 0 disarms the waiter's gate.  At most 32
+ * gates are armed at once (SFM_ERR_ARG beyond).  A pipelined caller arms it on
+ * the side stream right after the previous step's sweep, for its own main
+ * stream, so that sweep overlaps this step's correspondence build and
+ * five-point solve but not the scorer
  * (sfm_amd.pipeline.TwoViewHotPath.step_pipelined).  No reference
  * counterpart: the reference's steps are serial (essential_matrix.cu:190-280
  * then PSNet.py:130-158). */
-int sfm_score_gate(void* stream, int arm);
+int sfm_score_gate(void* stream, void* waiter, int arm);
 int sfm_plane_sweep_ref_planes(const float* ref, int batch, int channels, int h, int w, int nlabel, int out_dtype,
                                void* cost, void* workspace, size_t workspace_bytes, void* stream);
 int sfm_plane_sweep_psnet_warped_half(const float* ref, const float* tgt, int batch, int channels, int h, int w,
@@ -398,10 +403,19 @@ int sfm_conv3_f32(const float* in, int batch, int cin, int depth, int h, int w, 
  * k = 16 into fp32 accumulators (~2^-21 relative per product).  Same layouts
  * and arguments as sfm_conv3_f32, plus wexp in [-24, 24] (the caller picks it
  * so that 2^wexp max|w| < 2^15).  Replaces the same Conv3d layers
- * (models/PSNet.py:79-102, applied at 159-165). */
+ * (models/PSNet.py:79-102, applied at 159-165).
+ * The split is valid while every input activation is within the f16 range
+ * (|x| <= 65504; the reference's fp32 Conv3d has no such limit).  range_flag
+ * [dev] 4 bytes or NULL: when given, the call zeroes it, the kernel sets it to
+ * 1 if any input activation exceeds 65504 (or is infinite), and a second,
+ * stream-ordered launch of the sfm_conv3_f32 layer overwrites out in that case
+ * (its blocks exit at once otherwise) -- the layer's result is then exactly
+ * sfm_conv3_f32's.  NULL: no check (the caller guarantees the range).  Below
+ * 2^-14 the f16 terms are subnormal: such activations keep an absolute error
+ * <= 2^-25 per product term, not a relative one. */
 int sfm_conv3_f32x3(const float* in, int batch, int cin, int depth, int h, int w, const float* weights, int wexp,
                     const float* scale, const float* bias, const float* residual, int relu, int cout, float* out,
-                    void* stream);
+                    int* range_flag, void* stream);
 
 /* [batch][channels][plane] float32 (in_dtype 0) or bfloat16 (1) ->
  * [batch][plane][channels] float32 (channels a multiple of 4): the sweep's
@@ -434,11 +448,6 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     the line is not kept in the XCD's L2), 2 sc0
  *                                     sc1, 3 nt sc1; -1 (default): fp32 volumes 3,
  *                                     bf16 volumes 0; same bits
- *     "sweep_ref16"           0, 1    bf16 volumes with 16-byte stores and an even h*w:
- *                                     the reference rows copied from a bf16 copy
- *                                     k_tgt_quads makes once (1; measured ~1 % slower),
- *                                     or converted per plane from the fp32 rows (0,
- *                                     default); same bits
  *     "sweep_store_px"        -1,0,1, 16-byte lane stores of k_sweep_tile (8 bf16 / 4
  *                             2,4,8   fp32 consecutive pixels through a per-wave LDS
  *                                     stage) with that many pixels per lane for the

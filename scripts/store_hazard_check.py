@@ -13,11 +13,14 @@ STORE = re.compile(r"^(buffer|global|flat|scratch)_store_(dwordx3|dwordx4|b96|b1
 
 
 def vregs(tok):
-    m = re.match(r"v\[(\d+):(\d+)\]", tok)
+    """The vector registers an operand names, as (file, index) pairs: VGPRs
+    ('v', i) from v[i:j] / vN and AGPRs ('a', i) from a[i:j] / aN (a store
+    can take its data from AGPRs, and v_accvgpr_write / v_mfma write them)."""
+    m = re.match(r"([va])\[(\d+):(\d+)\]", tok)
     if m:
-        return set(range(int(m.group(1)), int(m.group(2)) + 1))
-    m = re.match(r"v(\d+)$", tok)
-    return {int(m.group(1))} if m else set()
+        return {(m.group(1), i) for i in range(int(m.group(2)), int(m.group(3)) + 1)}
+    m = re.match(r"([va])(\d+)$", tok)
+    return {(m.group(1), int(m.group(2)))} if m else set()
 
 
 def check(path, lines=None):

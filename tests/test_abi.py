@@ -164,7 +164,8 @@ def test_tuning_keys_round_trip():
     block = doc[doc.index("Tuning knobs"):doc.index("int sfm_tune_set")]
     keys = re.findall(r'"([a-z0-9_]+)"', block)
     assert set(keys) == set(_lib.tune_keys())           # documented == exported (sfm_tune_key)
-    assert len(set(keys)) == 30 and "score_mf_prune" in keys and "sweep_ref16" in keys and "score_lowp_template" in keys
+    assert len(set(keys)) == 29 and "score_mf_prune" in keys and "score_lowp_template" in keys
+    assert "sweep_ref16" not in keys          # the bf16 reference-row copy experiment is gone
     for k in keys:
         _lib.tune_get(k)
     old = _lib.tune_get("sweep_nj")
@@ -224,3 +225,37 @@ def test_no_store_data_overwrite_hazard():
     assert sum("buffer_store_dwordx4" in l for l in lines) > 0      # the sweep's wide stores are in there
     hits = H.check(_lib.LIB_PATH, lines)
     assert hits == [], hits[:3]
+
+
+def test_store_hazard_check_sees_vgpr_and_agpr_data():
+    """The checker itself on synthetic assembly: a 128-bit store whose data
+    VGPRs or AGPRs the next VALU instruction overwrites (v_mov / v_accvgpr_write
+    / v_mfma) is reported; a guarded pair (s_nop between) and a write to
+    other registers are not."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import store_hazard_check as H
+    asm = """_Z1kv:
+        buffer_store_dwordx4 v[4:7], v1, s[0:3], s4 offen
+        v_mov_b32_e32 v5, 0
+        buffer_store_dwordx4 a[8:11], v1, s[0:3], s4 offen
+        v_accvgpr_write_b32 a9, v2
+        global_store_dwordx4 v0, a[12:15], s[6:7]
+        v_mfma_f32_32x32x16_f16 a[0:15], v[20:23], v[24:27], a[0:15]
+        buffer_store_dwordx4 a[16:19], v1, s[0:3], s4 offen
+        s_nop 0
+        v_accvgpr_write_b32 a17, v2
+        buffer_store_dwordx4 v[8:11], v1, s[0:3], s4 offen
+        v_accvgpr_write_b32 a8, v2
+    """.split("\n")
+    hits = H.check(None, asm)
+    assert [h[2].split()[0] for h in hits] == ["v_mov_b32_e32", "v_accvgpr_write_b32", "v_mfma_f32_32x32x16_f16"]
+
+
+def test_reference_built_code_stays_in_the_build_container():
+    """oracle/_ref (the reference's own sources compiled here, for golden
+    generation only) never travels to the GPU box: .gpurunignore excludes it,
+    and excludes neither the product library nor the checker the GPU tests load."""
+    pats = [l.strip() for l in open(os.path.join(ROOT, ".gpurunignore")) if l.strip() and not l.startswith("#")]
+    assert "./oracle/_ref" in pats
+    for keep in ("./deep-sfm-revisited_amd", "./oracle", "*.so", "./oracle/liboracle_ransac.so", "./tests"):
+        assert keep not in pats, keep

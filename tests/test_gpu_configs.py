@@ -83,6 +83,26 @@ def test_c5_lo_ransac_8192_and_refinement(cuda):
     assert np.array_equal(E_opt.numpy(), R.optimise(p[:, :2], p[:, 2:], ref["E"], 1e-3, 0.0, 200))
 
 
+def test_c5_full_size_kitti_h8192_pruned_vs_oracle(cuda):
+    """C5 at full size: one KITTI pair (N = 435,032), H = 8192 (ransac_iter
+    16) through the default launch -- k_score_mf2 with count-bound pruning,
+    dispatch asserted -- against the oracle: winner, inlier count, E and P
+    (kernel_functions.cu:141-226, essential_matrix.cu:248-265)."""
+    from sfm_amd import _lib, ransac, synth
+    assert _lib.tune_get("score_mf") == 2 and _lib.tune_get("score_mf_prune") > 0
+    flow, K, _, _ = synth.kitti_pair_batch(1, seed=2024)
+    pts = _pts(flow, K, cuda)
+    assert pts.shape[1] == 435032
+    E, P, inl, win = ransac.ransac5_batched(pts, None, None, None, 16, 1e-4)
+    assert _lib.last_scorer() == "k_score_mf2+prune"
+    p = pts[0].cpu().numpy()
+    ref = R.ransac5(np.ascontiguousarray(p[:, :2]), np.ascontiguousarray(p[:, 2:]), iters=16, thr=1e-4,
+                    nthreads=16)
+    assert int(win[0]) == ref["winner"] and int(inl[0]) == ref["inliers"], (int(inl[0]), ref["inliers"])
+    assert np.array_equal(E[0].cpu().numpy(), ref["E"])
+    assert np.array_equal(P[0].cpu().numpy(), ref["P"])
+
+
 def test_c3_batch32_and_bf16(cuda):
     """32 pairs in one batched launch, each equal to the oracle; bf16 cost
     volume at batch 32 is the RNE rounding of the fp32 one."""

@@ -142,7 +142,7 @@ def test_score_gate_one_shot(cuda):
         with torch.cuda.stream(side):
             torch.cuda._sleep(sleep_cycles)
         if arm is not None:
-            assert lib.sfm_score_gate(ctypes.c_void_p(side.cuda_stream), arm) == 0
+            assert lib.sfm_score_gate(ctypes.c_void_p(side.cuda_stream), ctypes.c_void_p(main.cuda_stream), arm) == 0
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0.record(main)
         hp.pose(flow, K, Kinv)
@@ -158,3 +158,59 @@ def test_score_gate_one_shot(cuda):
     assert free < base + 20.0, (base, free)
     disarmed = timed_pose(sleep, 0)                          # arm = 0: nothing to wait for
     assert disarmed < base + 20.0, (base, disarmed)
+
+
+def test_score_gate_scoped_to_its_waiting_stream(cuda):
+    """The gate is armed for one waiting stream: a RANSAC call on another
+    stream of the same device (a second hot path, a plain computeP) neither
+    waits for it nor consumes it; the owner's next call still waits.  Outputs
+    are unchanged by the gating."""
+    import ctypes
+    import essential_matrix
+    from sfm_amd import _lib, synth
+    from sfm_amd.pipeline import TwoViewHotPath
+    lib = _lib.load()
+    B = 2
+    flow, K, _, _ = synth.kitti_pair_batch(B, seed=6, device=cuda)
+    owner = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 8, device=cuda)
+    other = TwoViewHotPath(B, (376, 1242), (94, 311), 32, 8, device=cuda)
+    Kinv = owner.k_inverse(K)
+    want = [t.clone() for t in owner.pose(flow, K, Kinv)]
+    q = owner.pts[0, :, :2].contiguous(); qp = owner.pts[0, :, 2:].contiguous()
+    E0, P0, n0 = essential_matrix.computeP(q, qp, 2000, 2000, 1, 1e-4)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream(device=cuda)
+    own_s = torch.cuda.Stream(device=cuda)
+    oth_s = torch.cuda.Stream(device=cuda)
+
+    def timed(stream, fn):
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(stream):
+            t0.record(stream)
+            out = fn()
+            t1.record(stream)
+        t1.synchronize()
+        return t0.elapsed_time(t1), out
+
+    base, _ = timed(own_s, lambda: owner.pose(flow, K, Kinv))
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(200_000_000)                       # ~0.1 s on the side stream
+    assert lib.sfm_score_gate(ctypes.c_void_p(side.cuda_stream), ctypes.c_void_p(own_s.cuda_stream), 1) == 0
+    # the other hot path and a plain computeP, each on its own stream: not held
+    t_other, got_other = timed(oth_s, lambda: other.pose(flow, K, Kinv))
+    assert t_other < base + 20.0, (base, t_other)
+    t_cp, got_cp = timed(oth_s, lambda: essential_matrix.computeP(q, qp, 2000, 2000, 1, 1e-4))
+    assert t_cp < base + 20.0, (base, t_cp)
+    # the owner's next call is still held (the gate was not consumed by them)
+    t_own, got_own = timed(own_s, lambda: owner.pose(flow, K, Kinv))
+    assert t_own > base + 20.0, (base, t_own)
+    torch.cuda.synchronize()
+    for a, b_ in zip(want, got_own):
+        assert torch.equal(a, b_)
+    for a, b_ in zip(want, got_other):
+        assert torch.equal(a, b_)
+    assert torch.equal(got_cp[0], E0) and torch.equal(got_cp[1], P0) and got_cp[2] == n0
+    # consumed: the owner's call after it runs free
+    t_free, _ = timed(own_s, lambda: owner.pose(flow, K, Kinv))
+    assert t_free < base + 20.0, (base, t_free)

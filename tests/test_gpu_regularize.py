@@ -320,7 +320,7 @@ def test_conv_layer_f32(cuda, B, cin, D, h, w, relu, resid, cout):
 # lo x lo term; an activation's lo term can be subnormal: 2^-24 absolute),
 # then the f32 accumulation as sfm_conv3_f32 -- the f32 layer bound holds.
 
-def _conv_f32x3(cuda, x, wt, scale, bias, res, relu, cout):
+def _conv_f32x3(cuda, x, wt, scale, bias, res, relu, cout, flag=None):
     from sfm_amd import _lib
     from sfm_amd.regularize import weight_exponent
     cin = x.shape[1]
@@ -337,7 +337,8 @@ def _conv_f32x3(cuda, x, wt, scale, bias, res, relu, cout):
     with torch.cuda.device(cuda):
         _lib.check(_lib.load().sfm_conv3_f32x3(_lib.ptr(xcl), B, cin, D, h, w, _lib.ptr(wp), e, _lib.ptr(sc),
                                                _lib.ptr(bi), None if rcl is None else _lib.ptr(rcl), 1 if relu else 0,
-                                               cout, _lib.ptr(out), _lib.stream_ptr(cuda)), "sfm_conv3_f32x3")
+                                               cout, _lib.ptr(out), None if flag is None else flag.data_ptr(),
+                                               _lib.stream_ptr(cuda)), "sfm_conv3_f32x3")
     out = out.cpu()
     return out.permute(0, 4, 1, 2, 3) if cout == 32 else out
 
@@ -374,6 +375,51 @@ def test_conv_layer_f32x3(cuda, B, cin, D, h, w, relu, resid, cout):
     e3 = float((got - want).norm() / want.norm())
     e32 = float((ref32 - want).norm() / want.norm())
     assert e3 <= 4 * e32 + 1e-7, (e3, e32)
+
+
+@pytest.mark.parametrize("peak,rerun", [(6.0e4, False), (7.0e4, True), (float("inf"), True)])
+def test_conv_layer_f32x3_out_of_f16_range(cuda, peak, rerun):
+    """An activation beyond the f16 maximum (65504) would make x_hi infinite:
+    with a range flag the layer detects it and re-runs as sfm_conv3_f32 in the
+    same call, so the output is exactly the fp32 layer's (finite where the
+    fp32 layer is); within range the flag stays clear and the split result
+    stands (the reference's fp32 Conv3d has no such limit)."""
+    g = torch.Generator().manual_seed(77)
+    B, cin, D, h, w, cout = 1, 32, 4, 9, 70, 32
+    x = torch.randn(B, cin, D, h, w, generator=g)
+    x[0, 3, 1, 4, 17] = peak
+    x[0, 9, 2, 0, 0] = -abs(peak) if peak != float("inf") else 5.0e4
+    wt = torch.randn(cout, cin, 3, 3, 3, generator=g) * 0.1
+    scale = 0.5 + torch.rand(cout, generator=g)
+    bias = 0.3 * torch.randn(cout, generator=g)
+    flag = torch.full((1,), 7, dtype=torch.int32, device=cuda)
+    got = _conv_f32x3(cuda, x, wt, scale, bias, None, True, cout, flag=flag)
+    ref32 = _conv_f32(cuda, x, wt, scale, bias, None, True, cout)
+    assert int(flag.item()) == (1 if rerun else 0)
+    if rerun:
+        assert torch.equal(torch.isnan(got), torch.isnan(ref32))
+        m = ~torch.isnan(ref32)
+        assert torch.equal(got[m], ref32[m])
+    else:
+        unguarded = _conv_f32x3(cuda, x, wt, scale, bias, None, True, cout)
+        assert torch.equal(got, unguarded) and bool(torch.isfinite(got).all())
+        mag = F.conv3d(x.abs().double(), wt.abs().double(), None, 1, 1) * scale.double().view(1, -1, 1, 1, 1)
+        err = (got.double() - ref32.double()).abs() - (4e-5 * mag + 1e-6)
+        assert float(err.max()) <= 0, float((got - ref32).abs().max())
+
+
+def test_stack_fp32x3_survives_large_activations(cuda):
+    """The fp32x3 stack on a cost volume scaled past the f16 range equals the
+    fp32 stack wherever a layer re-ran (here every layer: the activations
+    stay ~1e5) -- no inf / NaN from the split."""
+    m = _module(5, 64)
+    cost = torch.randn(1, 64, 8, 10, 24, generator=torch.Generator().manual_seed(3)) * 2.0e5
+    md = m.to(cuda)
+    got = md(cost.to(cuda), precision="fp32x3")
+    want = md(cost.to(cuda), precision="fp32")
+    assert bool(torch.isfinite(got).all())
+    r = float((got - want).norm() / want.norm())
+    assert r <= 2e-5, r                      # test_stack_f32x3_vs_oracle's bar
 
 
 @pytest.mark.parametrize("B,cin,L,h,w", [(1, 64, 16, 12, 20), (1, 32, 7, 5, 67)])

@@ -167,7 +167,7 @@ def test_shared_taps_equal_gathered(cuda, dtype, B, C, L, hw, tscale, by_depth):
     (2, 16, 8, (40, 300), 0.6, False),  # windows across row and plane ends
     (1, 8, 5, (13, 64), 1.0, False),    # hw < 256: windows span several planes
     (1, 8, 5, (13, 61), 1.0, False),    # odd slab: wide stores fall back to the plain path
-    (1, 8, 8, (13, 61), 1.0, False),    # odd h*w, slab a multiple of 8: wide stores, no bf16 reference copy
+    (1, 8, 8, (13, 61), 1.0, False),    # odd h*w, slab a multiple of 8: wide stores
     (2, 12, 6, (20, 96), 0.8, False),   # a partial channel group (C = 12, groups of 8)
 ])
 def test_wide_stores_equal_plain(cuda, dtype, B, C, L, hw, tscale, by_depth):
@@ -175,8 +175,7 @@ def test_wide_stores_equal_plain(cuda, dtype, B, C, L, hw, tscale, by_depth):
     pixels, transposed through a per-wave LDS stage, with px pixels per lane
     for the taps) writes the same bits as the plain 4-byte lane stores, with
     and without non-temporal stores, under every write-through policy
-    (sweep_store_wt), and (bf16) with the reference rows copied from
-    k_tgt_quads' bf16 copy or converted per plane (sweep_ref16)."""
+    (sweep_store_wt)."""
     from sfm_amd import _lib, synth
     from sfm_amd.sweep import plane_sweep_cost, quarter_intrinsics
     h, w = hw or synth.feature_hw()
@@ -187,18 +186,17 @@ def test_wide_stores_equal_plain(cuda, dtype, B, C, L, hw, tscale, by_depth):
     pose[:, :, 3] *= tscale / pose[:, :, 3].norm(dim=1, keepdim=True)
     K4, Ki4 = quarter_intrinsics(K, Ki)
     args = (ref.to(cuda), tgt.to(cuda), pose.to(cuda), K4.to(cuda), Ki4.to(cuda), L, 1.0)
-    # (store_px, store_nt, ref16, store_wt); the autouse fixture restores the tuning
+    # (store_px, store_nt, store_wt); the autouse fixture restores the tuning
     if dtype == torch.bfloat16:
-        cases = ((0, 2, 1, 0), (-1, 2, 1, -1), (-1, 2, 0, -1), (2, 2, 1, 1), (2, 2, 1, 3), (4, 2, 1, -1),
-                 (4, 2, 0, 2), (8, 2, 1, -1), (8, 0, 1, 3), (2, 0, 1, 0), (2, 0, 0, 0))
+        cases = ((0, 2, 0), (-1, 2, -1), (2, 2, 1), (2, 2, 3), (4, 2, -1), (4, 2, 2), (8, 2, -1), (8, 0, 3),
+                 (2, 0, 0))
     else:
-        cases = ((0, 2, 1, 0), (-1, 2, 1, -1), (1, 2, 1, 0), (1, 2, 1, 1), (1, 2, 1, 2), (2, 2, 1, -1),
-                 (4, 2, 1, 3), (1, 1, 1, 0), (2, 1, 1, 0))
+        cases = ((0, 2, 0), (-1, 2, -1), (1, 2, 0), (1, 2, 1), (1, 2, 2), (2, 2, -1), (4, 2, 3), (1, 1, 0),
+                 (2, 1, 0))
     outs = []
-    for px, nt, r16, wt in cases:
+    for px, nt, wt in cases:
         _lib.tune("sweep_store_px", px)
         _lib.tune("sweep_store_nt", nt)
-        _lib.tune("sweep_ref16", r16)
         _lib.tune("sweep_store_wt", wt)
         outs.append(plane_sweep_cost(*args, dtype=dtype, predict_by_depth=by_depth))
     bad = {}
