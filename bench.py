@@ -272,7 +272,7 @@ def profiled_pass(stepf, inputs, steps, dev):
 
 
 def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, traffic_src, rocprof=None,
-                   scorer=None):
+                   scorer=None, upper=None):
     """Roofline line of the RANSAC scoring kernel.  achieved = the algorithmic
     rate (SURVEY §8d: 50 FLOP per (candidate E, correspondence) evaluation);
     peak = the unit that executes it: the dense f16 MFMA peak for k_score_mf
@@ -281,8 +281,17 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
     pipe's own utilisation (4 MFMAs per 1024 evaluations): the kernel's floor."""
     work = (f"{done} evals x {FLOP_PER_EVAL} FLOP per launch: {cands} candidate E x N={n} = {evals}, "
             f"minus {skipped} skipped by exact count-bound pruning ({100.0 * skipped / max(evals, 1):.1f}%)")
+    issued_flop = done * MF_MFMA_FLOP_PER_EVAL
+    if upper is not None:
+        # the one-sided pruning (score_mf_prune_upper): every candidate's
+        # evaluations before the pruning point take the one-sided test (3 MFMAs
+        # per 32x32), the kept candidates are rescored two-sided over every point
+        one, two, kept = upper
+        issued_flop = one * MF_MFMA_FLOP_PER_EVAL * 3 // 4 + two * MF_MFMA_FLOP_PER_EVAL
+        work += (f"; one-sided pass (points not certainly outliers, upper-bound counts): {one} evals; "
+                 f"{kept} of {cands} candidates kept and rescored two-sided over every point: {two} evals")
     if use_mf:
-        issued = done * MF_MFMA_FLOP_PER_EVAL / (ms * 1e-3) / 1e12
+        issued = issued_flop / (ms * 1e-3) / 1e12
         rp = None
         if rocprof and rocprof[0]:
             t = done * FLOP_PER_EVAL / (rocprof[0] * 1e-3) / 1e12
@@ -295,7 +304,8 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
                 else "ransac_score (k_mf_cands + k_score_mf2)")
         return {"kernel": kern, "scorer": scorer, "bound": "mfma-f16", "achieved": round(tflops, 3),
                 "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_F16_TFLOPS, 4),
-                "mfma_issued": {"flop_per_eval": MF_MFMA_FLOP_PER_EVAL, "tflops": round(issued, 1),
+                "mfma_issued": {"flop_per_eval": MF_MFMA_FLOP_PER_EVAL if upper is None else "96 one-sided, 128 two-sided",
+                                "tflops": round(issued, 1),
                                 "frac": round(issued / PEAK_F16_TFLOPS, 4)},
                 "traffic": traffic, "traffic_source": traffic_src, "avg_launch_ms": round(ms, 4), "work": work,
                 "rocprof": rp, "valu_issue": valu_issue(pmc_kernel_counters(traffic_src, "ransac_score"))}
@@ -561,6 +571,11 @@ def _main_gpu(args, dist):
     evals = sum(cands) * hp.n                       # candidate E x correspondences per launch
     skipped = ransac.skipped_evaluations(hp.ws, B, args.iters)   # exact bound pruning (last launch)
     done = evals - skipped                          # evaluations the launch performed
+    upper_work = None
+    if _lib.last_scorer() == "k_score_mf2+prune" and _lib.tune_get("score_mf_prune_upper"):
+        kept, n1 = ransac.kept_candidates(hp.ws, B, args.iters, with_points=True)
+        one = sum(c * min(int(p), hp.n) for c, p in zip(cands, n1.tolist()))
+        upper_work = (one, int(kept.sum()) * hp.n, int(kept.sum()))
     score_ms = kt["ransac_score"]
     score_tflops = done * FLOP_PER_EVAL / (score_ms * 1e-3) / 1e12
     use_mf = bool(_lib.tune_get("score_mf")) and 2.0 ** -15 <= args.threshold < 1.0
@@ -611,7 +626,9 @@ def _main_gpu(args, dist):
             "roofline": score_roofline(use_mf, score_tflops, done, evals, skipped, sum(cands), hp.n, score_ms,
                                        traffic.get("ransac_score"), traffic_src,
                                        rocprof_kernel_ms(args, ("k_mf_cands", "k_score_mf2"),
-                                                         optional=("k_mf2_split", "k_mf2_lead", "k_mf2_keep")), _lib.last_scorer()),
+                                                         optional=("k_mf2_split", "k_mf2_lead", "k_mf2_keep",
+                                                                   "k_mf2_zero_kept")),
+                                       _lib.last_scorer(), upper_work),
             "roofline_sweep": {"kernel": "plane_sweep", "bound": "hbm", "achieved": round(sweep_gbs, 1),
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(sweep_gbs / PEAK_HBM_GBS, 4),
                                "traffic": traffic.get("plane_sweep"), "traffic_source": traffic_src,

@@ -1561,18 +1561,41 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
       // k_mf2_keep; C the kept candidates on the rest
       const int ch = tuning().score_mf_chunk;
       const int ch2 = tuning().score_mf_chunk2 ? tuning().score_mf_chunk2 : ch;
-      hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr, 0, ch);
+      // upper (score_mf_prune_upper, round 6): A and B run the one-sided
+      // test (counts = points not certainly outliers, upper bounds), the
+      // leader's count is exact over every point, and C scores the kept
+      // candidates two-sided over every span from zero counts
+      const bool up = tuning().score_mf_prune_upper != 0;
+      if (up)
+        hipLaunchKernelGGL((k_score_mf2<Src, false, true>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE,
+                           w.candF, w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr,
+                           0, ch);
+      else
+        hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF,
+                           w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr, 0, ch);
       hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, prune_pm, tuning().score_mf_prune_margin,
-                         w.cand_total, w.cntT, w.bnd);
-      hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
-                         kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
-      hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
-                         (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead);
+                         up ? tuning().score_mf_prune_beta : 0, w.cand_total, w.cntT, w.bnd);
+      if (up)
+        hipLaunchKernelGGL((k_score_mf2<Src, false, true>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE,
+                           w.candF, w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
+      else
+        hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF,
+                           w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
+      hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(up ? 4 * kLeadBlocks : kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
+                         (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead, up ? 1 : 0);
       hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax,
                          (const int32_t*)w.bnd, w.cand_total, w.cntT, w.lead, w.cmap, w.skipped);
-      hipLaunchKernelGGL((k_score_mf2<Src, true>), g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH, w.candE,
-                         w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap, 0, 0, (const int32_t*)w.bnd, 2, ch2);
+      if (up) {
+        hipLaunchKernelGGL(k_mf2_zero_kept, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax,
+                           (const int32_t*)w.lead, (const int32_t*)w.cmap, w.cntT);
+        hipLaunchKernelGGL((k_score_mf2<Src, true>), g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH,
+                           w.candE, w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap, 0, 1000,
+                           (const int32_t*)nullptr, 0, ch2);
+      } else {
+        hipLaunchKernelGGL((k_score_mf2<Src, true>), g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH,
+                           w.candE, w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap, 0, 0, (const int32_t*)w.bnd,
+                           2, ch2);
+      }
       set_last_scorer("k_score_mf2+prune");
     } else if (same && tuning().score_mf == 2) {
       hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF, w.cntT,
@@ -2166,6 +2189,20 @@ int sfm_ransac5_skipped_evaluations(const void* workspace, size_t workspace_byte
   Workspace w;
   layout((char*)workspace, bc, 0, iters, &w);
   SFM_HIP(hipMemcpy(skipped_host, w.skipped, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return SFM_OK;
+}
+
+int sfm_ransac5_kept_candidates(const void* workspace, size_t workspace_bytes, int batch, int iters,
+                                int32_t* kept_host, int32_t* points_host) {
+  SFM_REQUIRE(workspace && kept_host && batch >= 1 && batch <= SFM_MAX_BATCH && iters >= 1, "invalid arguments");
+  SFM_REQUIRE(workspace_bytes >= layout(nullptr, batch, 0, iters, nullptr), "workspace too small");
+  Workspace w;
+  layout((char*)workspace, batch, 0, iters, &w);
+  SFM_HIP(hipMemcpy(kept_host, w.lead + 3 * SFM_MAX_BATCH, sizeof(int32_t) * batch, hipMemcpyDeviceToHost));
+  if (points_host) {
+    SFM_HIP(hipMemcpy(points_host, w.bnd + 2 * SFM_MAX_BATCH, sizeof(int32_t) * batch, hipMemcpyDeviceToHost));
+    for (int b = 0; b < batch; ++b) points_host[b] *= kMf2Span;   // spans -> points (the caller clamps at N)
+  }
   return SFM_OK;
 }
 

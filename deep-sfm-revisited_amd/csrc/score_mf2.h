@@ -41,6 +41,10 @@ constexpr int kMf2Span = 1024;                 // points per staged span
 constexpr int kMf2Tiles = kMf2Span / 32;       // tiles per span (every run decides all of them)
 constexpr int kMf2Guide = 2;                   // a claim takes remainder / (guide x blocks per XCD)
 constexpr int kMf2Queue = 128;                 // undecided entries per wave and drain window (LDS)
+#ifndef SFM_MF2_WQ
+#define SFM_MF2_WQ 1                           // the two-phase (word, then lane-parallel bit) queue build
+#endif
+constexpr int kMf2WordSlots = kMf2Queue / 2;   // word slots (two words each) of the two-phase build
 // candidate tiles the LDS count table holds (tiles past it publish per run)
 constexpr int kMf2TblTiles = 352;
 constexpr int kMf2TblWords = kMf2TblTiles * kKC / 2;   // 16-bit counts, two per word
@@ -127,6 +131,18 @@ __device__ __forceinline__ void mf2_signs(const MfZ& r, uint32_t (&s1)[16], uint
   }
 }
 
+// the upper-bound (one-sided) form: z2 alone and its sign bits
+__device__ __forceinline__ mf_float16 mf2_zhi(mf_half8 bd, mf_half8 NH, const mf_float16& a) {
+  mf_float16 aa;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) aa[g] = a[g] * a[g];
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(NH, bd, aa, 0, 0, 0);
+}
+__device__ __forceinline__ void mf2_signs_hi(const mf_float16& z2, uint32_t (&s2)[16]) {
+#pragma unroll
+  for (int g = 0; g < 16; ++g) s2[g] = __builtin_amdgcn_alignbit(s2[g], __float_as_uint(z2[g]), 31);
+}
+
 // queue entry (candidate row << 24 | span-relative point) of the lowest set
 // bit j of a string: bit j = tile kMf2Tiles - 1 - j
 __device__ __forceinline__ uint32_t mf2_qbase(int g, int hl, int rl) {
@@ -153,7 +169,11 @@ __device__ __forceinline__ int32_t* mf2_count_slot(int32_t* cntT, const int32_t*
   return cntT + (size_t)b * cmax + (cmap ? cmap[i] : j);
 }
 
-template <class Src, bool kMap>
+// kUpper (round 6): the one-sided pass of count-bound pruning -- z2 only (3
+// MFMAs and 32 VALU per tile instead of 4 and 48), each count the number of
+// points NOT certainly outliers (sign of z2), an upper bound on the inlier
+// count; no undecided queue, no float64 drain.
+template <class Src, bool kMap, bool kUpper = false>
 __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(kMf2Wpe, kMf2Wpe))) void k_score_mf2(
     const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
     const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
@@ -328,7 +348,27 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         uint32_t s1[16], s2[16];
 #pragma unroll
         for (int g = 0; g < 16; ++g) { s1[g] = 0u; s2[g] = 0u; }
-        {
+        if constexpr (kUpper) {
+          // the same pipeline with z2 alone: a(t+1) MFMAs, z2(t), sign bits of z2(t-1)
+          const mf_half8 NH = -AH;
+          mf_float16 aA = mf2_a(mf2_load_ab(fr, mf2_lane()), A1, A2), aB;
+          mf_float16 zA, zB;
+          aB = mf2_a(mf2_load_ab(fr + (size_t)1 * kTileHalves, mf2_lane()), A1, A2);
+          zA = mf2_zhi(mf2_load_d(fr, mf2_lane()), NH, aA);
+#pragma unroll 1
+          for (int t = 1; t < kMf2Tiles - 1; t += 2) {
+            const _Float16* lp = fr + (size_t)t * kTileHalves + (size_t)mf2_lane() * 8;
+            aA = mf2_a(mf2_load_ab(lp + kTileHalves, 0), A1, A2);
+            zB = mf2_zhi(mf2_load_d(lp, 0), NH, aB);
+            mf2_signs_hi(zA, s2);
+            aB = mf2_a(mf2_load_ab(lp + 2 * kTileHalves, 0), A1, A2);
+            zA = mf2_zhi(mf2_load_d(lp + kTileHalves, 0), NH, aA);
+            mf2_signs_hi(zB, s2);
+          }
+          zB = mf2_zhi(mf2_load_d(fr + (size_t)(kMf2Tiles - 1) * kTileHalves, mf2_lane()), NH, aB);
+          mf2_signs_hi(zA, s2);
+          mf2_signs_hi(zB, s2);
+        } else {
           // step t: a(t+1) MFMAs, aa(t) -> z(t) MFMAs, sign bits of z(t-1)
           // (step 0 and the last step peeled; pairs of steps ping-pong the
           // a / z register sets)
@@ -359,6 +399,11 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
         // the next run's rows load under this run's queue, drain and reduction
         const int kn = claim_tile();
         if (kn < k1) load_rows(b, kn, ctot);
+        if constexpr (kUpper) {
+          // not-certain-outlier bits are the count: s1 := s2, nothing undecided
+#pragma unroll
+          for (int g = 0; g < 16; ++g) s1[g] = s2[g];
+        } else {
         // 3. undecided evaluations -> the queue -> float64.  Bit j of a string
         // is tile kMf2Tiles-1-j, point 32 (kMf2Tiles-1-j) + rl of the span.
         int nl = 0;
@@ -374,6 +419,39 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 #endif
         const double* Epair = candE + (size_t)b * cmax * kCandStride;
         const int32_t* mpair = cmap ? cmap + (size_t)b * cmax : nullptr;
+#if SFM_MF2_WQ
+        if (qtotal <= kMf2WordSlots) {
+          // Two-phase build (round 6): (1) every lane appends its non-empty
+          // undecided words as (word, entry base) pairs -- no per-bit loop --
+          // at its first bit's queue position (the wave scan of the bit
+          // counts), leaving a hole for each further bit; (2) lane i expands
+          // the word at slot i, if any, into entries i, i+1, ... (lane-parallel:
+          // the per-bit loop runs as many times as the fullest word has bits).
+          uint32_t* qw = queue;                              // 64 slots of two words, then 4-byte entries
+          qw[2 * lane] = 0u;                                 // holes: an empty word
+          int pos = incl - nl;
+#pragma unroll
+          for (int g = 0; g < 16; ++g) {
+            const uint32_t uu = mf2_undecided(s1[g], s2[g]);
+            if (uu) {
+              qw[2 * pos] = uu;
+              qw[2 * pos + 1] = mf2_qbase(g, hl, rl);
+              pos += __popc(uu);
+            }
+          }
+          wave_sync();
+          uint32_t uu = qw[2 * lane];
+          const uint32_t top = qw[2 * lane + 1];
+          wave_sync();                                       // every slot read before the entries overwrite them
+          for (int p = lane; uu; ++p) {
+            qw[p] = mf2_qentry(top, uu);
+            uu &= uu - 1u;
+          }
+          wave_sync();
+          mf2_drain(Epair, mpair, c0, s_pts, kc, lane, cnt, queue, qtotal);
+          wave_sync();
+        } else
+#endif
         for (int base = 0; base < qtotal; base += kMf2Queue) {
           int pos = incl - nl - base;
           if (qtotal <= kMf2Queue) {
@@ -402,6 +480,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
           wave_sync();
           mf2_drain(Epair, mpair, c0, s_pts, kc, lane, cnt, queue, min(kMf2Queue, qtotal - base));
           wave_sync();
+        }
         }
         // 4. counts: popcounts of the inlier strings over the 32 points of each half + the float64 counts
         int cT[16];
@@ -487,7 +566,11 @@ __device__ __forceinline__ int mf2_n1(const PairParams& pp, int b, const int32_t
 // boundaries bnd[0..3][b] = 0, sA, sB, spans for the launches A [0, sA), B
 // [sA, sB) (every candidate) and, after k_mf2_lead / k_mf2_keep at sB, C
 // [sB, spans) (the kept candidates).
-__global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int pm, int margin,
+// beta (per mille, the one-sided pruning of round 6; 0: the rule above):
+// the pass before the pruning point is cheap there, so the point moves on
+// to where only candidates with inlier ratio >= beta rho can still be kept,
+// f = (1 - rho) / (1 - beta rho) (+ margin).
+__global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int pm, int margin, int beta,
                                                    const int32_t* __restrict__ cand_total,
                                                    const int32_t* __restrict__ cntT, int32_t* __restrict__ bnd) {
   __shared__ int s_max[16];
@@ -509,6 +592,8 @@ __global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int
   // f = 1 - rho + margin in per mille, rounded up; >= pm; > 990: no pruning
   const long long rho_pm = nA > 0 ? ((long long)mx * 1000) / nA : 0;
   long long f = 1000 - rho_pm + margin;
+  if (beta > 0 && rho_pm < 1000)
+    f = (1000000 * (1000 - rho_pm) + (1000000 - beta * rho_pm) - 1) / (1000000 - beta * rho_pm) + margin;
   f = max(f, (long long)pm);
   const int sB = f > 990 ? all : max(sA, mf2_span_at(all, (int)f));
   bnd[0 * SFM_MAX_BATCH + b] = 0;
@@ -517,16 +602,19 @@ __global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int
   bnd[3 * SFM_MAX_BATCH + b] = all;
 }
 
+// full (the one-sided pruning of round 6, whose counts are upper bounds):
+// the leader's exact count over every point [0, M), its partial count
+// recorded as 0, so that lb = lead[0] + lead[2] is still its exact count.
 template <class Src>
 __global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp, int cmax, const int32_t* __restrict__ bnd,
                                                   const int32_t* __restrict__ cand_total,
                                                   const double* __restrict__ candE, const int32_t* __restrict__ cntT,
-                                                  ScoreConsts kc, int32_t* __restrict__ lead) {
+                                                  ScoreConsts kc, int32_t* __restrict__ lead, int full) {
   __shared__ unsigned long long s_key[16];
   __shared__ int s_part[16];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int M = max(pp.test[b], pp.rtest[b]);
-  const int n1 = mf2_n1(pp, b, bnd);
+  const int n1 = full ? 0 : mf2_n1(pp, b, bnd);
   const int ctot = cand_total[b];
   if (ctot <= 0) return;
   const int32_t* cnt = cntT + (size_t)b * cmax;
@@ -562,7 +650,7 @@ __global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp,
     int r = 0;
     for (int w = 0; w < 16; ++w) r += s_part[w];
     if (blockIdx.x == 0) {
-      lead[0 * SFM_MAX_BATCH + b] = (int)(key >> 32);
+      lead[0 * SFM_MAX_BATCH + b] = full ? 0 : (int)(key >> 32);
       lead[1 * SFM_MAX_BATCH + b] = ld;
     }
     if (r) atomicAdd(&lead[2 * SFM_MAX_BATCH + b], r);
@@ -614,4 +702,15 @@ __global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, cons
     if (skipped && live > tot)
       atomicAdd(skipped, (unsigned long long)(live - tot) * (unsigned long long)(M - n1));
   }
+}
+
+// After k_mf2_keep in the one-sided pruning: the kept candidates' (upper
+// bound) counts are zeroed, so that the two-sided launch over every span
+// leaves their exact counts in cntT (a separate launch: k_mf2_keep's blocks
+// read every count below their range while they run).
+__global__ __launch_bounds__(256) void k_mf2_zero_kept(int cmax, const int32_t* __restrict__ lead,
+                                                      const int32_t* __restrict__ cmap, int32_t* __restrict__ cntT) {
+  const int b = blockIdx.y;
+  const int j = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (j < lead[3 * SFM_MAX_BATCH + b]) cntT[(size_t)b * cmax + cmap[(size_t)b * cmax + j]] = 0;
 }

@@ -32,6 +32,8 @@ _SIGS = [
       _c_dp]),
     ("sfm_ransac5_candidate_counts", ctypes.c_int,
      [_c_dp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]),
+    ("sfm_ransac5_kept_candidates", ctypes.c_int,
+     [_c_dp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _c_dp, _c_dp]),
     ("sfm_ransac5_skipped_evaluations", ctypes.c_int,
      [_c_dp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
     ("sfm_pack_points", ctypes.c_int, [_c_dp, _c_dp, ctypes.c_int64, _c_dp, _c_dp]),

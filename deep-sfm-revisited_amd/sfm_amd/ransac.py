@@ -243,6 +243,18 @@ def skipped_evaluations(workspace, batch, iters):
     return int(out.value)
 
 
+def kept_candidates(workspace, batch, iters, with_points=False):
+    """Per pair, the candidates the last pruned k_score_mf2 call kept (scored
+    to their exact counts) and, with_points, its pruning point (points scored
+    before it, a multiple of 1024: clamp at N); synchronises.  Undefined after
+    an unpruned call."""
+    out = torch.zeros(batch, dtype=torch.int32)
+    pts = torch.zeros(batch, dtype=torch.int32)
+    _lib.check(_lib.load().sfm_ransac5_kept_candidates(_lib.ptr(workspace), workspace.numel(), int(batch), int(iters),
+                                                       _lib.ptr(out), _lib.ptr(pts)), "sfm_ransac5_kept_candidates")
+    return (out, pts) if with_points else out
+
+
 KEYPOINT_MODES = {"round": 0, "sample_sp": 1, "sift_pose": 2}
 
 

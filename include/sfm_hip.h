@@ -174,6 +174,14 @@ int sfm_ransac5_candidate_counts(const void* workspace, size_t workspace_bytes, 
  * winner (ransac5.hip, PruneState). */
 int sfm_ransac5_skipped_evaluations(const void* workspace, size_t workspace_bytes, int batch, int iters,
                                     unsigned long long* skipped_host);
+/* Diagnostics of the last pruned k_score_mf2 call on the workspace
+ * (sfm_last_scorer() "k_score_mf2+prune"): per pair, the candidates the
+ * count bound kept (scored to their exact counts); every other candidate was
+ * dropped after the pruning point; points_host (optional): per pair, the
+ * pruning point in points (a multiple of the 1024-point span: clamp at the
+ * pair's N).  Undefined after an unpruned call.  Synchronises. */
+int sfm_ransac5_kept_candidates(const void* workspace, size_t workspace_bytes, int batch, int iters,
+                                int32_t* kept_host, int32_t* points_host);
 
 /* Pack reference-layout q, qp (n x 2 each) into pts (n x 4). */
 int sfm_pack_points(const double* q, const double* qp, int64_t n, double* pts_out, void* stream);
@@ -483,6 +491,18 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     num_test == num_ransac_test, no per-
  *                                     hypothesis scores, >= 32 spans per pair
  *     "score_mf_prune_margin" 0..200  that margin, per mille (10)
+ *     "score_mf_prune_upper"  0, 1    the launches before the pruning point run
+ *                                     the one-sided test (counts of the points
+ *                                     not certainly outliers: upper bounds), the
+ *                                     leader is counted exactly over every point
+ *                                     and the kept candidates are scored two-
+ *                                     sided over every span (1, default); 0: the
+ *                                     two-sided counts throughout (round 5).
+ *                                     Winner, count, E, P unchanged either way
+ *     "score_mf_prune_beta"   0..990  with score_mf_prune_upper: the pruning point
+ *                                     f = (1 - rho) / (1 - beta rho) + margin, where
+ *                                     only candidates of inlier ratio >= beta rho
+ *                                     can survive (per mille, 800); 0: 1 - rho + margin
  *     "roots_split"           0, 1, 2 k_roots_split: falsi nodes shared by the wave's
  *                                     64 lanes (1, default), or by the four waves of
  *                                     a block (2, measured 2-6 % slower), speculated

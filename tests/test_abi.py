@@ -164,7 +164,8 @@ def test_tuning_keys_round_trip():
     block = doc[doc.index("Tuning knobs"):doc.index("int sfm_tune_set")]
     keys = re.findall(r'"([a-z0-9_]+)"', block)
     assert set(keys) == set(_lib.tune_keys())           # documented == exported (sfm_tune_key)
-    assert len(set(keys)) == 29 and "score_mf_prune" in keys and "score_lowp_template" in keys
+    assert len(set(keys)) == 31 and "score_mf_prune" in keys and "score_lowp_template" in keys
+    assert "score_mf_prune_upper" in keys
     assert "sweep_ref16" not in keys          # the bf16 reference-row copy experiment is gone
     for k in keys:
         _lib.tune_get(k)

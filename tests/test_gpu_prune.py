@@ -24,7 +24,11 @@ pytestmark = pytest.mark.gpu
 
 
 def _both(pts, n=None, iters=2, thr=1e-4, nt=None, nr=None, scorer="mf2"):
-    """{0: unpruned, 1: pruned} -> (E, P, inliers, winner, skipped evaluations)."""
+    """{0: unpruned, 1: pruned (k_score_mf2: the round-6 one-sided passes,
+    score_mf_prune_upper = 1, the default), 2 (k_score_mf2 only): pruned with
+    the round-5 two-sided passes} -> (E, P, inliers, winner, skipped
+    evaluations, kept candidates (k_score_mf2 pruned: summed over the pairs;
+    else None), candidates)."""
     from sfm_amd import _lib, ransac
     B = pts.shape[0]
     ws = ransac.workspace_for(B, iters, pts.device)
@@ -32,24 +36,28 @@ def _both(pts, n=None, iters=2, thr=1e-4, nt=None, nr=None, scorer="mf2"):
     snap = _lib.tune_snapshot()
     try:
         _lib.tune("score_mf", 2 if scorer == "mf2" else 0)
-        for prune in (0, 1):
+        for prune in ((0, 1, 2) if scorer == "mf2" else (0, 1)):
             if scorer == "mf2":
                 _lib.tune("score_mf_prune", 880 if prune else 0)
+                _lib.tune("score_mf_prune_upper", 0 if prune == 2 else 1)
             else:
                 _lib.tune("score_prune", prune)
             E, P, inl, win = ransac.ransac5_batched(pts, n, nt, nr, iters, thr, workspace=ws)
             torch.cuda.synchronize()
             kernels[prune] = _lib.last_scorer()
-            out[prune] = (E.cpu(), P.cpu(), inl.cpu(), win.cpu(), ransac.skipped_evaluations(ws, B, iters))
+            kept = (int(ransac.kept_candidates(ws, B, iters).sum()) if scorer == "mf2" and prune else None)
+            out[prune] = (E.cpu(), P.cpu(), inl.cpu(), win.cpu(), ransac.skipped_evaluations(ws, B, iters), kept,
+                          int(sum(ransac.candidate_counts(ws, B, iters))))
     finally:
         _lib.tune_restore(snap)
     return out, kernels
 
 
 def _same(out):
-    a, b = out[0], out[1]
-    for x, y in zip(a[:4], b[:4]):
-        assert torch.equal(x, y)
+    a = out[0]
+    for k in out:
+        for x, y in zip(a[:4], out[k][:4]):
+            assert torch.equal(x, y), k
     assert a[4] == 0
 
 
@@ -61,11 +69,15 @@ def test_pruning_full_size_kitti(cuda, scorer):
     pts = ransac.flow_to_points(flow, torch.inverse(K))
     out, kernels = _both(pts, iters=8, scorer=scorer)
     if scorer == "mf2":
-        assert kernels == {0: "k_score_mf2", 1: "k_score_mf2+prune"}
+        assert kernels == {0: "k_score_mf2", 1: "k_score_mf2+prune", 2: "k_score_mf2+prune"}
     else:
         assert kernels == {0: "k_score32", 1: "k_score32+prune"}
     _same(out)
-    assert out[1][4] > 0                                  # pruning engaged on real data
+    if scorer == "mf2":                                   # pruning engaged on real data:
+        assert out[1][5] < 0.5 * out[1][6]                #   the one-sided form kept under half the candidates,
+        assert out[2][4] > 0                              #   the two-sided form skipped evaluations
+    else:
+        assert out[1][4] > 0
     assert int(out[1][2].min()) > 10000
 
 
@@ -80,16 +92,20 @@ def test_mf2_pruning_full_size_vs_oracle(cuda):
     _same(out)
     p = pts[0].cpu().numpy()
     ref = R.ransac5(p[:, :2], p[:, 2:], iters=8, thr=1e-4, nthreads=16)
-    E, P, inl, win, skipped = out[1]
+    E, P, inl, win, _, kept, ncand = out[1]
     assert int(win[0]) == ref["winner"] and int(inl[0]) == ref["inliers"]
     assert np.array_equal(E[0].numpy(), ref["E"]) and np.array_equal(P[0].numpy(), ref["P"])
     total = int(ref["hyp_ncand"].clip(min=1).sum()) * p.shape[0]
-    print(f"skipped {skipped} of {total} evaluations ({100.0 * skipped / total:.1f} %)")
+    skipped = out[2][4]                                   # the round-5 two-sided form
+    print(f"two-sided form: skipped {skipped} of {total} evaluations ({100.0 * skipped / total:.1f} %); "
+          f"one-sided form: kept {kept} of {ncand} candidates")
     assert skipped > 0.03 * total
+    assert kept < 0.5 * ncand
 
 
+@pytest.mark.parametrize("upper", [1, 0])
 @pytest.mark.parametrize("pm,margin", [(500, 25), (800, 0), (990, 25), (850, 200), (600, 100)])
-def test_mf2_pruning_split_points(cuda, pm, margin):
+def test_mf2_pruning_split_points(cuda, pm, margin, upper):
     """Other first-launch shares and margins (the keys' ranges, including a
     pruning point past 990: no pruning): the same results."""
     from sfm_amd import _lib, ransac, synth
@@ -98,6 +114,7 @@ def test_mf2_pruning_split_points(cuda, pm, margin):
     ref = ransac.ransac5_batched(pts, None, None, None, 2, 1e-3, return_scores=True)
     _lib.tune("score_mf_prune", pm)
     _lib.tune("score_mf_prune_margin", margin)
+    _lib.tune("score_mf_prune_upper", upper)
     got = ransac.ransac5_batched(pts, None, None, None, 2, 1e-3)
     assert _lib.last_scorer() == "k_score_mf2+prune"
     for x, y in zip(got, ref[:4]):
@@ -115,7 +132,7 @@ def test_pruning_matches_oracle_winner(cuda, seed, scorer):
     _same(out)
     p = pts[0].cpu().numpy()
     ref = R.ransac5(np.ascontiguousarray(p[:, :2]), np.ascontiguousarray(p[:, 2:]), iters=2, thr=1e-4, nthreads=16)
-    E, P, inl, win, _ = out[1]
+    E, P, inl, win = out[1][:4]
     assert int(win[0]) == ref["winner"] and int(inl[0]) == ref["inliers"]
     assert np.array_equal(E[0].numpy(), ref["E"])
     assert np.array_equal(P[0].numpy(), ref["P"])
@@ -169,4 +186,4 @@ def test_mf2_pruning_adapts_to_the_indoor_inlier_ratio(cuda):
     _same(out)
     N = pts.shape[1]
     assert 0.05 < int(out[1][2].max()) / N < 0.12                 # the regime the test is about
-    assert out[1][4] > 0
+    assert out[2][4] > 0 and out[1][5] < 0.5 * out[1][6]
