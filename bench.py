@@ -289,7 +289,7 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
         one, two, kept = upper
         issued_flop = one * MF_MFMA_FLOP_PER_EVAL * 3 // 4 + two * MF_MFMA_FLOP_PER_EVAL
         work += (f"; one-sided pass (points not certainly outliers, upper-bound counts): {one} evals; "
-                 f"{kept} of {cands} candidates kept and rescored two-sided over every point: {two} evals")
+                 f"{kept} of {cands} candidates kept and counted exactly over every point (float64, or two-sided past 256 per pair): {two} evals")
     if use_mf:
         issued = issued_flop / (ms * 1e-3) / 1e12
         rp = None

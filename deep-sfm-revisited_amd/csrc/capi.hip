@@ -128,7 +128,7 @@ const TuneKey kTuneKeys[] = {
     {"score_mf_chunk", &sfm::Tuning::score_mf_chunk, [](int v) { return v >= 1 && v <= 4096; }},
     {"score_mf_prune_margin", &sfm::Tuning::score_mf_prune_margin, [](int v) { return v >= 0 && v <= 200; }},
     {"score_mf_prune_upper", &sfm::Tuning::score_mf_prune_upper, v_01},
-    {"score_mf_prune_beta", &sfm::Tuning::score_mf_prune_beta, [](int v) { return v >= 0 && v <= 990; }},
+    {"score_mf_exact_max", &sfm::Tuning::score_mf_exact_max, [](int v) { return v >= 0 && v <= 256; }},
     {"score_mf_blocks_per_cu", &sfm::Tuning::score_mf_blocks_per_cu, [](int v) { return v >= 1 && v <= 8; }},
     {"score_interleave", &sfm::Tuning::score_interleave, v_01},
     {"conv_rolling", &sfm::Tuning::conv_rolling, v_01},

@@ -40,7 +40,7 @@ struct Tuning {
                                  // k_mf2_split (an empty middle launch when the pair's own point is not later)
   int score_mf_prune_margin = 10; // the pruning point: 1 - (inlier ratio) + margin, per mille (k_mf2_split)
   int score_mf_prune_upper = 1;   // pruning passes one-sided (upper-bound counts), the kept candidates rescored (round 6)
-  int score_mf_prune_beta = 800;  // with upper: the pruning point where only ratios >= beta rho survive (per mille)
+  int score_mf_exact_max = 256;   // with upper: kept candidates per pair counted in float64 (k_mf2_exact); more: MFMA
   int score_mf_chunk = 64;       // k_score_mf2: smallest unit range a block claims (32-candidate tiles of a span);
                                  // 64 measured ~1 % faster than 128 with pruning (profiles/r05_prune_ab.txt)
   int score_mf_blocks_per_cu = 1; // k_score_mf persistent grid (LDS: one block per CU)

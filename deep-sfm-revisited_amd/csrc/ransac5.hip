@@ -73,7 +73,8 @@ struct Workspace {
   unsigned long long* skipped;  // [1] evaluations skipped by pruning (whole call)
   unsigned long long* claim;    // [9] k_score_mf2's range-claim counters and finished-block count (zero between launches)
   int32_t* cmap;       // [B][Cmax] k_mf2_keep: the kept candidates of each pair
-  int32_t* lead;       // [4][64] k_mf2_lead / _keep: leader count, index, rest count, kept candidates
+  int32_t* lead;       // [5][64] k_mf2_lead / _keep: leader count, index, rest count, kept candidates,
+                       // kept candidates left to the matrix-core pass (one-sided pruning)
   int32_t* bnd;        // [4][64] k_mf2_split: span boundaries of the pruned launches per pair
   double* pack;        // [n_max][4] (last: its size is the only n_max-dependent one)
 };
@@ -107,7 +108,7 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   // field it uses must sit at an offset independent of n_max
   t.claim = (unsigned long long*)take(kMf2ClaimBytes);
   t.cmap = (int32_t*)take(bc * C * 4);
-  t.lead = (int32_t*)take(SFM_MAX_BATCH * 4 * 4);
+  t.lead = (int32_t*)take(SFM_MAX_BATCH * 5 * 4);
   t.bnd = (int32_t*)take(SFM_MAX_BATCH * 4 * 4);
   t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
   if (w) *w = t;
@@ -1553,7 +1554,7 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
     hipLaunchKernelGGL(k_mf_cands, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax, w.cand_total, w.candE,
                        w.candF, mp, w.claim, prune_pm > 0 ? w.lead : nullptr);
     const dim3 gmf(std::max(1, cus) * tuning().score_mf_blocks_per_cu);
-    const dim3 g2(std::max(1, cus)), b2(kMf2Waves * 64);
+    const dim3 g2(std::max(1, cus)), b2(kMf2Waves * 64), b2u(mf2_waves<true>() * 64);
     if (same && tuning().score_mf == 2 && prune_pm > 0) {
       // count-bound pruning: A every candidate on the first prune_pm per mille
       // of each pair's spans; k_mf2_split picks the pair's pruning point sB
@@ -1561,37 +1562,43 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
       // k_mf2_keep; C the kept candidates on the rest
       const int ch = tuning().score_mf_chunk;
       const int ch2 = tuning().score_mf_chunk2 ? tuning().score_mf_chunk2 : ch;
-      // upper (score_mf_prune_upper, round 6): A and B run the one-sided
-      // test (counts = points not certainly outliers, upper bounds), the
-      // leader's count is exact over every point, and C scores the kept
-      // candidates two-sided over every span from zero counts
-      const bool up = tuning().score_mf_prune_upper != 0;
-      if (up)
-        hipLaunchKernelGGL((k_score_mf2<Src, false, true>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE,
-                           w.candF, w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr,
+      if (tuning().score_mf_prune_upper) {
+        // the one-sided pruning (round 6): A every candidate on every span
+        // with the one-sided test (counts = points not certainly outliers:
+        // upper bounds); k_mf2_split with its point at the end; k_mf2_lead the
+        // leader's exact count over every point (lb); k_mf2_keep the
+        // candidates whose upper count reaches lb; their counts zeroed, then
+        // counted exactly -- float64 (k_mf2_exact) for pairs with at most
+        // kExactMaxKept of them, the two-sided matrix-core pass through the
+        // index map for the others (lead row 4: their kept counts, else 0)
+        hipLaunchKernelGGL((k_score_mf2<Src, false, true>), g2, b2u, 0, s, src, pp, bc, cmax, w.cand_total, w.candE,
+                           w.candF, w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 1000, (const int32_t*)nullptr,
                            0, ch);
-      else
-        hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF,
-                           w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr, 0, ch);
-      hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, prune_pm, tuning().score_mf_prune_margin,
-                         up ? tuning().score_mf_prune_beta : 0, w.cand_total, w.cntT, w.bnd);
-      if (up)
-        hipLaunchKernelGGL((k_score_mf2<Src, false, true>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE,
-                           w.candF, w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
-      else
-        hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF,
-                           w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
-      hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(up ? 4 * kLeadBlocks : kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
-                         (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead, up ? 1 : 0);
-      hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax,
-                         (const int32_t*)w.bnd, w.cand_total, w.cntT, w.lead, w.cmap, w.skipped);
-      if (up) {
+        hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, 1000, 0, w.cand_total, w.cntT, w.bnd);
+        hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(4 * kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
+                           (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead, 1);
+        hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax,
+                           (const int32_t*)w.bnd, w.cand_total, w.cntT, w.lead, w.cmap, w.skipped,
+                           tuning().score_mf_exact_max);
         hipLaunchKernelGGL(k_mf2_zero_kept, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax,
                            (const int32_t*)w.lead, (const int32_t*)w.cmap, w.cntT);
-        hipLaunchKernelGGL((k_score_mf2<Src, true>), g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH,
+        hipLaunchKernelGGL(k_mf2_exact<Src>, dim3(kExactBlocks, bc), dim3(256), 0, s, src, pp, cmax,
+                           (const int32_t*)w.lead, (const int32_t*)w.cmap, w.candE, kc, w.cntT,
+                           tuning().score_mf_exact_max);
+        hipLaunchKernelGGL((k_score_mf2<Src, true>), g2, b2, 0, s, src, pp, bc, cmax, w.lead + 4 * SFM_MAX_BATCH,
                            w.candE, w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap, 0, 1000,
                            (const int32_t*)nullptr, 0, ch2);
       } else {
+        hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF,
+                           w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr, 0, ch);
+        hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, prune_pm,
+                           tuning().score_mf_prune_margin, w.cand_total, w.cntT, w.bnd);
+        hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF,
+                           w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
+        hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
+                           (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead, 0);
+        hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax,
+                           (const int32_t*)w.bnd, w.cand_total, w.cntT, w.lead, w.cmap, w.skipped, 0);
         hipLaunchKernelGGL((k_score_mf2<Src, true>), g2, b2, 0, s, src, pp, bc, cmax, w.lead + 3 * SFM_MAX_BATCH,
                            w.candE, w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap, 0, 0, (const int32_t*)w.bnd,
                            2, ch2);

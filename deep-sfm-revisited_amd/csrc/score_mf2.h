@@ -37,6 +37,12 @@
 // and the profiles/r0*_mf2_* A/B records; their code is gone.
 constexpr int kMf2Waves = 12;                  // 3 per SIMD, two accumulator sets
 constexpr int kMf2Wpe = kMf2Waves / 4;
+// the one-sided pass (kUpper) holds fewer registers (z2 alone): its block
+// size, waves per SIMD = SFM_MF2_UP_WAVES / 4
+#ifndef SFM_MF2_UP_WAVES
+#define SFM_MF2_UP_WAVES 16
+#endif
+template <bool kUpper> constexpr int mf2_waves() { return kUpper ? SFM_MF2_UP_WAVES : kMf2Waves; }
 constexpr int kMf2Span = 1024;                 // points per staged span
 constexpr int kMf2Tiles = kMf2Span / 32;       // tiles per span (every run decides all of them)
 constexpr int kMf2Guide = 2;                   // a claim takes remainder / (guide x blocks per XCD)
@@ -174,7 +180,8 @@ __device__ __forceinline__ int32_t* mf2_count_slot(int32_t* cntT, const int32_t*
 // points NOT certainly outliers (sign of z2), an upper bound on the inlier
 // count; no undecided queue, no float64 drain.
 template <class Src, bool kMap, bool kUpper = false>
-__global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(kMf2Wpe, kMf2Wpe))) void k_score_mf2(
+__global__ __launch_bounds__(mf2_waves<kUpper>() * 64)
+__attribute__((amdgpu_waves_per_eu(mf2_waves<kUpper>() / 4, mf2_waves<kUpper>() / 4))) void k_score_mf2(
     const Src src, PairParams pp, int batch, int cmax, const int32_t* __restrict__ cand_total,
     const double* __restrict__ candE, const _Float16* __restrict__ candF, int32_t* __restrict__ cntT,
     ScoreConsts kc, unsigned long long* __restrict__ claim, const int32_t* __restrict__ cmap_arg, int sp_lo,
@@ -184,8 +191,9 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   __shared__ __attribute__((aligned(16))) _Float16 s_frag[kMf2Tiles][3][64][8];
   __shared__ double4 s_pts[kMf2Span];
   __shared__ int32_t s_tbl[kMf2TblWords];                    // the block's counts of pair tb's candidates
-  __shared__ uint32_t s_queue[kMf2Waves][kMf2Queue];
-  __shared__ int32_t s_cnt[kMf2Waves][kKC];                  // float64 drain counts
+  constexpr int NW = mf2_waves<kUpper>();
+  __shared__ uint32_t s_queue[kUpper ? 1 : NW][kMf2Queue];   // (the one-sided pass: neither queue nor drain)
+  __shared__ int32_t s_cnt[kUpper ? 1 : NW][kKC];           // float64 drain counts
   __shared__ long long s_first[SFM_MAX_BATCH + 1];           // first unit of each pair
   __shared__ int32_t s_tiles[SFM_MAX_BATCH];                 // candidate tiles per pair
   __shared__ int32_t s_ctot[SFM_MAX_BATCH];
@@ -214,14 +222,14 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
     }
     s_first[batch] = acc;
   }
-  for (int i = tid; i < kMf2Waves * kKC; i += kMf2Waves * 64) (&s_cnt[0][0])[i] = 0;
-  for (int i = tid; i < kMf2TblWords; i += kMf2Waves * 64) s_tbl[i] = 0;
+  for (int i = tid; i < (kUpper ? 1 : NW) * kKC; i += NW * 64) (&s_cnt[0][0])[i] = 0;
+  for (int i = tid; i < kMf2TblWords; i += NW * 64) s_tbl[i] = 0;
   int tb = -1;                                               // the pair the table holds (block-uniform)
   int tspans = 0;                                            // spans added since the last flush
   // the table to pair fb's global counts (all threads, between block barriers)
   auto flush = [&](int fb) {
     const int nt = min(s_tiles[fb], kMf2TblTiles) * kKC;
-    for (int i = tid; i < nt / 2; i += kMf2Waves * 64) {
+    for (int i = tid; i < nt / 2; i += NW * 64) {
       const uint32_t v = (uint32_t)s_tbl[i];
       if (v) {
         if (v & 0xffffu) atomicAdd(mf2_count_slot(cntT, cmap, fb, cmax, 2 * i), (int)(v & 0xffffu));
@@ -244,8 +252,8 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
   const int xcd = (int)(blockIdx.x % (unsigned)nx);
   const int per_x = G / nx;
   int victim = 0;                                            // XCDs after our own already drained
-  int32_t* cnt = s_cnt[wv];
-  uint32_t* queue = s_queue[wv];
+  int32_t* cnt = s_cnt[kUpper ? 0 : wv];
+  uint32_t* queue = s_queue[kUpper ? 0 : wv];
   const _Float16* fr = &s_frag[0][0][0][0];
   constexpr int kTileHalves = 3 * 64 * 8;
   int b = 0;
@@ -323,10 +331,10 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
       ++tspans;
       // 1. stage the span: B fragments for every slot (dead slots: the decided-outlier sentinel)
       if (tid == 0) s_claim = 0;
-      for (int i = tid; i < kMf2Span; i += kMf2Waves * 64) {
+      for (int i = tid; i < kMf2Span; i += NW * 64) {
         const bool live = i < np;
         const double4 v = src.load(b, live ? p0 + i : p0);
-        s_pts[i] = v;
+        if constexpr (!kUpper) s_pts[i] = v;                 // (the float64 points serve the drain only)
         mf_stage_point(v, live, &s_frag[i >> 5][0][0][0], i & 31);
       }
       lds_barrier();
@@ -546,6 +554,7 @@ __global__ __launch_bounds__(kMf2Waves * 64) __attribute__((amdgpu_waves_per_eu(
 // index, 2: its rest count (zeroed by k_mf_cands at the start of the scoring
 // phase), 3: kept candidates (the second launch's cand_total).
 constexpr int kLeadBlocks = 32;
+constexpr int kExactMaxKept = 256;   // kept candidates per pair k_mf2_exact can count (score_mf_exact_max)
 
 // the points the launches before the pruning scored: spans [0, bnd[2][b])
 __device__ __forceinline__ int mf2_n1(const PairParams& pp, int b, const int32_t* bnd) {
@@ -566,11 +575,9 @@ __device__ __forceinline__ int mf2_n1(const PairParams& pp, int b, const int32_t
 // boundaries bnd[0..3][b] = 0, sA, sB, spans for the launches A [0, sA), B
 // [sA, sB) (every candidate) and, after k_mf2_lead / k_mf2_keep at sB, C
 // [sB, spans) (the kept candidates).
-// beta (per mille, the one-sided pruning of round 6; 0: the rule above):
-// the pass before the pruning point is cheap there, so the point moves on
-// to where only candidates with inlier ratio >= beta rho can still be kept,
-// f = (1 - rho) / (1 - beta rho) (+ margin).
-__global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int pm, int margin, int beta,
+// (The one-sided pruning of round 6 runs it with pm = 1000: its pruning point
+// is the end of the pair, sA = sB = spans.)
+__global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int pm, int margin,
                                                    const int32_t* __restrict__ cand_total,
                                                    const int32_t* __restrict__ cntT, int32_t* __restrict__ bnd) {
   __shared__ int s_max[16];
@@ -592,8 +599,6 @@ __global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int
   // f = 1 - rho + margin in per mille, rounded up; >= pm; > 990: no pruning
   const long long rho_pm = nA > 0 ? ((long long)mx * 1000) / nA : 0;
   long long f = 1000 - rho_pm + margin;
-  if (beta > 0 && rho_pm < 1000)
-    f = (1000000 * (1000 - rho_pm) + (1000000 - beta * rho_pm) - 1) / (1000000 - beta * rho_pm) + margin;
   f = max(f, (long long)pm);
   const int sB = f > 990 ? all : max(sA, mf2_span_at(all, (int)f));
   bnd[0 * SFM_MAX_BATCH + b] = 0;
@@ -660,7 +665,8 @@ __global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp,
 __global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, const int32_t* __restrict__ bnd,
                                                   const int32_t* __restrict__ cand_total,
                                                   const int32_t* __restrict__ cntT, int32_t* __restrict__ lead,
-                                                  int32_t* __restrict__ cmap, unsigned long long* __restrict__ skipped) {
+                                                  int32_t* __restrict__ cmap, unsigned long long* __restrict__ skipped,
+                                                  int exact_max) {
   __shared__ int s_part[16];
   __shared__ int s_before[16];
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -697,11 +703,56 @@ __global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, cons
     cmap[(size_t)b * cmax + off] = c;
   }
   if (tid == 0) {
-    if (c0 + 1024 >= ctot) lead[3 * SFM_MAX_BATCH + b] = base + tot;   // the last block: the kept count
+    if (c0 + 1024 >= ctot) {                                  // the last block: the kept count
+      lead[3 * SFM_MAX_BATCH + b] = base + tot;
+      // the one-sided pruning: a pair with more kept candidates than the
+      // float64 kernel takes goes to the two-sided matrix-core pass
+      lead[4 * SFM_MAX_BATCH + b] = base + tot > exact_max ? base + tot : 0;
+    }
     const int live = min(1024, ctot - c0);
     if (skipped && live > tot)
       atomicAdd(skipped, (unsigned long long)(live - tot) * (unsigned long long)(M - n1));
   }
+}
+
+// k_mf2_exact (the one-sided pruning, after k_mf2_zero_kept): the kept
+// candidates' exact counts over every point with the drain's float64 test,
+// for pairs with at most kExactMaxKept of them (the others: k_score_mf2 over
+// every span through the index map).  Block (x, b) takes the x-th slice of
+// pair b's points; every wave tests its points against each kept candidate in
+// turn (E through uniform loads), the count of the wave's inliers goes to an
+// LDS table by one lane, the table to cntT once per block.
+constexpr int kExactBlocks = 64;     // blocks per pair
+
+template <class Src>
+__global__ __launch_bounds__(256) void k_mf2_exact(const Src src, PairParams pp, int cmax,
+                                                   const int32_t* __restrict__ lead, const int32_t* __restrict__ cmap,
+                                                   const double* __restrict__ candE, ScoreConsts kc,
+                                                   int32_t* __restrict__ cntT, int exact_max) {
+  __shared__ int32_t s_cnt[kExactMaxKept];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int kept = lead[3 * SFM_MAX_BATCH + b];
+  if (kept <= 0 || kept > exact_max) return;
+  for (int c = tid; c < kept; c += 256) s_cnt[c] = 0;
+  __syncthreads();
+  const int M = max(pp.test[b], pp.rtest[b]);
+  const int k0 = (int)((long long)M * blockIdx.x / gridDim.x);
+  const int k1 = (int)((long long)M * (blockIdx.x + 1) / gridDim.x);
+  const int32_t* mp = cmap + (size_t)b * cmax;
+  const double* Eb = candE + (size_t)b * cmax * kCandStride;
+  const int lane = tid & 63;
+  for (int k = k0 + tid; k < k1; k += 256) {
+    const double4 v = src.load(b, k);
+    const int first = __builtin_amdgcn_readfirstlane(lane);     // the wave's first active lane
+#pragma unroll 1
+    for (int j = 0; j < kept; ++j) {
+      const unsigned long long m = __ballot(inlier_f64v(Eb + (size_t)mp[j] * kCandStride, v, kc));
+      if (lane == first && m) atomicAdd(&s_cnt[j], (int)__popcll(m));
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < kept; c += 256)
+    if (s_cnt[c]) atomicAdd(cntT + (size_t)b * cmax + mp[c], s_cnt[c]);
 }
 
 // After k_mf2_keep in the one-sided pruning: the kept candidates' (upper

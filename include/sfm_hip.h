@@ -491,18 +491,19 @@ int sfm_to_channels_last_f32(const void* in, int in_dtype, int batch, int channe
  *                                     num_test == num_ransac_test, no per-
  *                                     hypothesis scores, >= 32 spans per pair
  *     "score_mf_prune_margin" 0..200  that margin, per mille (10)
- *     "score_mf_prune_upper"  0, 1    the launches before the pruning point run
- *                                     the one-sided test (counts of the points
- *                                     not certainly outliers: upper bounds), the
- *                                     leader is counted exactly over every point
- *                                     and the kept candidates are scored two-
- *                                     sided over every span (1, default); 0: the
- *                                     two-sided counts throughout (round 5).
- *                                     Winner, count, E, P unchanged either way
- *     "score_mf_prune_beta"   0..990  with score_mf_prune_upper: the pruning point
- *                                     f = (1 - rho) / (1 - beta rho) + margin, where
- *                                     only candidates of inlier ratio >= beta rho
- *                                     can survive (per mille, 800); 0: 1 - rho + margin
+ *     "score_mf_prune_upper"  0, 1    1 (default, round 6): every candidate on
+ *                                     every point with the one-sided test (counts
+ *                                     of the points not certainly outliers: upper
+ *                                     bounds), the leader counted exactly, and only
+ *                                     the candidates whose upper count reaches it
+ *                                     counted exactly (float64, or the two-sided
+ *                                     matrix-core pass past 256 per pair); 0: the
+ *                                     round-5 two-sided passes with the pruning
+ *                                     point above.  Winner, count, E, P unchanged
+ *     "score_mf_exact_max"    0..256  with score_mf_prune_upper: pairs with at most
+ *                                     this many kept candidates count them in
+ *                                     float64 (k_mf2_exact), the others on the
+ *                                     matrix cores (256; same counts either way)
  *     "roots_split"           0, 1, 2 k_roots_split: falsi nodes shared by the wave's
  *                                     64 lanes (1, default), or by the four waves of
  *                                     a block (2, measured 2-6 % slower), speculated

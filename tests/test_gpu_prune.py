@@ -187,3 +187,26 @@ def test_mf2_pruning_adapts_to_the_indoor_inlier_ratio(cuda):
     N = pts.shape[1]
     assert 0.05 < int(out[1][2].max()) / N < 0.12                 # the regime the test is about
     assert out[2][4] > 0 and out[1][5] < 0.5 * out[1][6]
+
+
+@pytest.mark.parametrize("exact_max", [256, 4, 0])
+def test_mf2_one_sided_exact_count_paths(cuda, exact_max):
+    """The one-sided pruning counts the kept candidates exactly in float64
+    (k_mf2_exact, pairs with at most score_mf_exact_max kept) or on the matrix
+    cores (the two-sided k_score_mf2 through the index map, the other pairs):
+    either way winner, count, E and P equal the unpruned run's, on KITTI-size
+    pairs (2 pairs, full size) where both paths can occur in one batch."""
+    from sfm_amd import _lib, ransac, synth
+    flow, K, _, _ = synth.kitti_pair_batch(2, seed=77, device=cuda)
+    pts = ransac.flow_to_points(flow, torch.inverse(K))
+    ref = ransac.ransac5_batched(pts, None, None, None, 4, 1e-4, return_scores=True)
+    assert _lib.last_scorer() == "k_score_mf2"
+    ws = ransac.workspace_for(2, 4, pts.device)
+    _lib.tune("score_mf_prune_upper", 1)
+    _lib.tune("score_mf_exact_max", exact_max)
+    got = ransac.ransac5_batched(pts, None, None, None, 4, 1e-4, workspace=ws)
+    assert _lib.last_scorer() == "k_score_mf2+prune"
+    for x, y in zip(got, ref[:4]):
+        assert torch.equal(x, y)
+    kept = ransac.kept_candidates(ws, 2, 4)
+    assert int(kept.min()) >= 1 and int(kept.sum()) < 0.1 * sum(ransac.candidate_counts(ws, 2, 4))
