@@ -573,9 +573,11 @@ def _main_gpu(args, dist):
     done = evals - skipped                          # evaluations the launch performed
     upper_work = None
     if _lib.last_scorer() == "k_score_mf2+prune" and _lib.tune_get("score_mf_prune_upper"):
-        kept, n1 = ransac.kept_candidates(hp.ws, B, args.iters, with_points=True)
-        one = sum(c * min(int(p), hp.n) for c, p in zip(cands, n1.tolist()))
-        upper_work = (one, int(kept.sum()) * hp.n, int(kept.sum()))
+        # every evaluation not skipped took the one-sided test (all candidates
+        # before the pruning point, the first keep's survivors after it); the
+        # finally kept candidates were then counted exactly over every point
+        kept = ransac.kept_candidates(hp.ws, B, args.iters)
+        upper_work = (done, int(kept.sum()) * hp.n, int(kept.sum()))
     score_ms = kt["ransac_score"]
     score_tflops = done * FLOP_PER_EVAL / (score_ms * 1e-3) / 1e12
     use_mf = bool(_lib.tune_get("score_mf")) and 2.0 ** -15 <= args.threshold < 1.0

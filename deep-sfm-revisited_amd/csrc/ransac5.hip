@@ -73,6 +73,7 @@ struct Workspace {
   unsigned long long* skipped;  // [1] evaluations skipped by pruning (whole call)
   unsigned long long* claim;    // [9] k_score_mf2's range-claim counters and finished-block count (zero between launches)
   int32_t* cmap;       // [B][Cmax] k_mf2_keep: the kept candidates of each pair
+  int32_t* cmap2;      // [B][Cmax] k_mf2_keep_map: those kept again at the end (one-sided pruning)
   int32_t* lead;       // [5][64] k_mf2_lead / _keep: leader count, index, rest count, kept candidates,
                        // kept candidates left to the matrix-core pass (one-sided pruning)
   int32_t* bnd;        // [4][64] k_mf2_split: span boundaries of the pruned launches per pair
@@ -108,6 +109,7 @@ static size_t layout(char* base, int bc, int64_t n_max, int iters, Workspace* w)
   // field it uses must sit at an offset independent of n_max
   t.claim = (unsigned long long*)take(kMf2ClaimBytes);
   t.cmap = (int32_t*)take(bc * C * 4);
+  t.cmap2 = (int32_t*)take(bc * C * 4);
   t.lead = (int32_t*)take(SFM_MAX_BATCH * 5 * 4);
   t.bnd = (int32_t*)take(SFM_MAX_BATCH * 4 * 4);
   t.pack = (double*)take((size_t)std::max<int64_t>(n_max, 0) * 4 * 8);
@@ -1533,6 +1535,7 @@ struct ScoreBufs {
   int32_t* cntT;
   int32_t* cntR;
   unsigned long long* claim;   // [9] k_score_mf2's range-claim counters and finished-block count
+  int32_t* cmap2 = nullptr;    // the one-sided pruning's second keep (k_mf2_keep_map)
   int32_t* cmap = nullptr;     // count-bound pruning (k_mf2_lead / _keep): kept candidates, the
   int32_t* lead = nullptr;     // leader records (their [3] = kept candidates), the evaluations skipped,
   unsigned long long* skipped = nullptr;
@@ -1563,36 +1566,47 @@ static void score_dispatch(const Src& src, const PairParams& pp, int bc, int cma
       const int ch = tuning().score_mf_chunk;
       const int ch2 = tuning().score_mf_chunk2 ? tuning().score_mf_chunk2 : ch;
       if (tuning().score_mf_prune_upper) {
-        // the one-sided pruning (round 6): A every candidate on every span
-        // with the one-sided test (counts = points not certainly outliers:
-        // upper bounds); k_mf2_split with its point at the end; k_mf2_lead the
-        // leader's exact count over every point (lb); k_mf2_keep the
-        // candidates whose upper count reaches lb; their counts zeroed, then
-        // counted exactly -- float64 (k_mf2_exact) for pairs with at most
-        // kExactMaxKept of them, the two-sided matrix-core pass through the
-        // index map for the others (lead row 4: their kept counts, else 0)
+        // the one-sided pruning (round 6), counts = points not certainly
+        // outliers (upper bounds):
+        //   A every candidate one-sided on the first prune_pm per mille of the
+        //     spans; k_mf2_split the pair's pruning point sB (round 5's rule)
+        //     and the leader (the first max); B every candidate up to sB;
+        //   k_mf2_lead the leader's exact count over every point (lb);
+        //   k_mf2_keep the candidates whose upper bound (count + points left)
+        //     reaches lb; A2 those one-sided on the rest; k_mf2_keep_map those
+        //     whose full upper count still reaches lb;
+        //   their counts zeroed, then counted exactly: float64 (k_mf2_exact)
+        //   for pairs with at most score_mf_exact_max of them, the two-sided
+        //   matrix-core pass through the index map for the others (lead row 4)
         hipLaunchKernelGGL((k_score_mf2<Src, false, true>), g2, b2u, 0, s, src, pp, bc, cmax, w.cand_total, w.candE,
-                           w.candF, w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 1000, (const int32_t*)nullptr,
-                           0, ch);
-        hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, 1000, 0, w.cand_total, w.cntT, w.bnd);
+                           w.candF, w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, prune_pm,
+                           (const int32_t*)nullptr, 0, ch);
+        hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, prune_pm,
+                           tuning().score_mf_prune_margin, w.cand_total, w.cntT, w.bnd, w.lead);
+        hipLaunchKernelGGL((k_score_mf2<Src, false, true>), g2, b2u, 0, s, src, pp, bc, cmax, w.cand_total, w.candE,
+                           w.candF, w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
         hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(4 * kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
-                           (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead, 1);
+                           (const int32_t*)w.bnd, w.cand_total, w.candE, w.cntT, kc, w.lead, 2);
         hipLaunchKernelGGL(k_mf2_keep, dim3((cmax + 1023) / 1024, bc), dim3(1024), 0, s, pp, cmax,
-                           (const int32_t*)w.bnd, w.cand_total, w.cntT, w.lead, w.cmap, w.skipped,
-                           tuning().score_mf_exact_max);
+                           (const int32_t*)w.bnd, w.cand_total, w.cntT, w.lead, w.cmap, w.skipped, 0);
+        hipLaunchKernelGGL((k_score_mf2<Src, true, true>), g2, b2u, 0, s, src, pp, bc, cmax,
+                           w.lead + 3 * SFM_MAX_BATCH, w.candE, w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap,
+                           0, 0, (const int32_t*)w.bnd, 2, ch2);
+        hipLaunchKernelGGL(k_mf2_keep_map, dim3(bc), dim3(1024), 0, s, cmax, (const int32_t*)w.cntT, w.lead,
+                           (const int32_t*)w.cmap, w.cmap2, tuning().score_mf_exact_max);
         hipLaunchKernelGGL(k_mf2_zero_kept, dim3((cmax + 255) / 256, bc), dim3(256), 0, s, cmax,
-                           (const int32_t*)w.lead, (const int32_t*)w.cmap, w.cntT);
-        hipLaunchKernelGGL(k_mf2_exact<Src>, dim3(kExactBlocks, bc), dim3(256), 0, s, src, pp, cmax,
-                           (const int32_t*)w.lead, (const int32_t*)w.cmap, w.candE, kc, w.cntT,
+                           (const int32_t*)w.lead, (const int32_t*)w.cmap2, w.cntT);
+        hipLaunchKernelGGL(k_mf2_exact<Src>, dim3(kExactBlocks, bc), dim3(kExactThreads), 0, s, src, pp, cmax,
+                           (const int32_t*)w.lead, (const int32_t*)w.cmap2, w.candE, kc, w.cntT,
                            tuning().score_mf_exact_max);
         hipLaunchKernelGGL((k_score_mf2<Src, true>), g2, b2, 0, s, src, pp, bc, cmax, w.lead + 4 * SFM_MAX_BATCH,
-                           w.candE, w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap, 0, 1000,
+                           w.candE, w.candF, w.cntT, kc, w.claim, (const int32_t*)w.cmap2, 0, 1000,
                            (const int32_t*)nullptr, 0, ch2);
       } else {
         hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF,
                            w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, prune_pm, (const int32_t*)nullptr, 0, ch);
         hipLaunchKernelGGL(k_mf2_split, dim3(bc), dim3(1024), 0, s, pp, cmax, prune_pm,
-                           tuning().score_mf_prune_margin, w.cand_total, w.cntT, w.bnd);
+                           tuning().score_mf_prune_margin, w.cand_total, w.cntT, w.bnd, (int32_t*)nullptr);
         hipLaunchKernelGGL((k_score_mf2<Src, false>), g2, b2, 0, s, src, pp, bc, cmax, w.cand_total, w.candE, w.candF,
                            w.cntT, kc, w.claim, (const int32_t*)nullptr, 0, 0, (const int32_t*)w.bnd, 1, ch);
         hipLaunchKernelGGL(k_mf2_lead<Src>, dim3(kLeadBlocks, bc), dim3(1024), 0, s, src, pp, cmax,
@@ -1904,6 +1918,7 @@ static int run_chunk(const Src& src, const int64_t* n, int bc, int num_test,
     ProfScope ps("ransac_score", s);
     ScoreBufs sb{w.cand_total, w.candE, w.candF, w.cntT, w.cntR, w.claim};
     sb.cmap = w.cmap;
+    sb.cmap2 = w.cmap2;
     sb.lead = w.lead;
     sb.bnd = w.bnd;
     sb.skipped = w.skipped;

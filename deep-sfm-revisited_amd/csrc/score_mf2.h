@@ -222,6 +222,11 @@ __attribute__((amdgpu_waves_per_eu(mf2_waves<kUpper>() / 4, mf2_waves<kUpper>() 
     }
     s_first[batch] = acc;
   }
+  __syncthreads();
+  // nothing to score (the one-sided pruning's matrix-core pass when every
+  // pair's kept candidates went to k_mf2_exact): out before the table set-up.
+  // No block claims a unit, so the counters stay as the last launch left them.
+  if (s_first[batch] == 0) return;
   for (int i = tid; i < (kUpper ? 1 : NW) * kKC; i += NW * 64) (&s_cnt[0][0])[i] = 0;
   for (int i = tid; i < kMf2TblWords; i += NW * 64) s_tbl[i] = 0;
   int tb = -1;                                               // the pair the table holds (block-uniform)
@@ -577,10 +582,14 @@ __device__ __forceinline__ int mf2_n1(const PairParams& pp, int b, const int32_t
 // [sB, spans) (the kept candidates).
 // (The one-sided pruning of round 6 runs it with pm = 1000: its pruning point
 // is the end of the pair, sA = sB = spans.)
+// leader (the one-sided pruning, counts final): also the leader -- the first
+// candidate with the largest count, as k_mf2_lead picks it -- into lead rows
+// 0 (0: the partial count of a full count) and 1 (its index).
 __global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int pm, int margin,
                                                    const int32_t* __restrict__ cand_total,
-                                                   const int32_t* __restrict__ cntT, int32_t* __restrict__ bnd) {
-  __shared__ int s_max[16];
+                                                   const int32_t* __restrict__ cntT, int32_t* __restrict__ bnd,
+                                                   int32_t* __restrict__ leader) {
+  __shared__ unsigned long long s_key[16];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int M = max(pp.test[b], pp.rtest[b]);
   const int all = mf2_spans(M);
@@ -588,14 +597,26 @@ __global__ __launch_bounds__(1024) void k_mf2_split(PairParams pp, int cmax, int
   const int nA = min(sA * kMf2Span, M);
   const int ctot = cand_total[b];
   const int32_t* cnt = cntT + (size_t)b * cmax;
-  int mx = 0;
-  for (int c = tid; c < ctot; c += 1024) mx = max(mx, cnt[c]);
+  // key = count << 32 | ~c: the max is the first of the largest
+  unsigned long long key = 0ull;
+  for (int c = tid; c < ctot; c += 1024) {
+    const unsigned long long k = ((unsigned long long)(uint32_t)cnt[c] << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)c);
+    key = k > key ? k : key;
+  }
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
-  if (lane == 0) s_max[wv] = mx;
+  for (int d = 32; d >= 1; d >>= 1) {
+    const unsigned long long o = __shfl_xor(key, d, 64);
+    key = o > key ? o : key;
+  }
+  if (lane == 0) s_key[wv] = key;
   __syncthreads();
   if (tid != 0) return;
-  for (int w = 0; w < 16; ++w) mx = max(mx, s_max[w]);
+  for (int w = 0; w < 16; ++w) key = s_key[w] > key ? s_key[w] : key;
+  int mx = (int)(key >> 32);
+  if (leader && ctot > 0) {
+    leader[0 * SFM_MAX_BATCH + b] = 0;
+    leader[1 * SFM_MAX_BATCH + b] = (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull));
+  }
   // f = 1 - rho + margin in per mille, rounded up; >= pm; > 990: no pruning
   const long long rho_pm = nA > 0 ? ((long long)mx * 1000) / nA : 0;
   long long f = 1000 - rho_pm + margin;
@@ -623,6 +644,25 @@ __global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp,
   const int ctot = cand_total[b];
   if (ctot <= 0) return;
   const int32_t* cnt = cntT + (size_t)b * cmax;
+  if (full == 2) {
+    // the leader from k_mf2_split (lead rows 0 / 1): its exact count alone
+    const int ldr = lead[1 * SFM_MAX_BATCH + b];
+    const int k0 = (int)((long long)M * blockIdx.x / gridDim.x);
+    const int k1 = (int)((long long)M * (blockIdx.x + 1) / gridDim.x);
+    const double* El = candE + ((size_t)b * cmax + ldr) * kCandStride;
+    int r = 0;
+    for (int k = k0 + tid; k < k1; k += blockDim.x) r += inlier_f64v(El, src.load(b, k), kc) ? 1 : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) r += __shfl_xor(r, d, 64);
+    if (lane == 0) s_part[wv] = r;
+    __syncthreads();
+    if (tid == 0) {                                          // one global atomic per block
+      int t = 0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_part[w];
+      if (t) atomicAdd(&lead[2 * SFM_MAX_BATCH + b], t);
+    }
+    return;
+  }
   // the leader (key count << 32 | ~c: the first of the largest); every block
   // finds the same one
   unsigned long long key = 0ull;
@@ -722,37 +762,81 @@ __global__ __launch_bounds__(1024) void k_mf2_keep(PairParams pp, int cmax, cons
 // pair b's points; every wave tests its points against each kept candidate in
 // turn (E through uniform loads), the count of the wave's inliers goes to an
 // LDS table by one lane, the table to cntT once per block.
-constexpr int kExactBlocks = 64;     // blocks per pair
+constexpr int kExactBlocks = 128;    // blocks per pair
+constexpr int kExactThreads = 1024;  // (latency-bound: every point a dependent float64 chain)
 
 template <class Src>
-__global__ __launch_bounds__(256) void k_mf2_exact(const Src src, PairParams pp, int cmax,
+__global__ __launch_bounds__(kExactThreads) void k_mf2_exact(const Src src, PairParams pp, int cmax,
                                                    const int32_t* __restrict__ lead, const int32_t* __restrict__ cmap,
                                                    const double* __restrict__ candE, ScoreConsts kc,
                                                    int32_t* __restrict__ cntT, int exact_max) {
   __shared__ int32_t s_cnt[kExactMaxKept];
+  __shared__ double s_E[kExactMaxKept][10];                   // the kept candidates' E and guard constant
   const int b = blockIdx.y, tid = threadIdx.x;
   const int kept = lead[3 * SFM_MAX_BATCH + b];
   if (kept <= 0 || kept > exact_max) return;
-  for (int c = tid; c < kept; c += 256) s_cnt[c] = 0;
+  const int32_t* mp = cmap + (size_t)b * cmax;
+  const double* Eb = candE + (size_t)b * cmax * kCandStride;
+  for (int c = tid; c < kept; c += kExactThreads) s_cnt[c] = 0;
+  for (int i = tid; i < kept * 10; i += kExactThreads) s_E[i / 10][i % 10] = Eb[(size_t)mp[i / 10] * kCandStride + i % 10];
   __syncthreads();
   const int M = max(pp.test[b], pp.rtest[b]);
   const int k0 = (int)((long long)M * blockIdx.x / gridDim.x);
   const int k1 = (int)((long long)M * (blockIdx.x + 1) / gridDim.x);
-  const int32_t* mp = cmap + (size_t)b * cmax;
-  const double* Eb = candE + (size_t)b * cmax * kCandStride;
   const int lane = tid & 63;
-  for (int k = k0 + tid; k < k1; k += 256) {
+  for (int k = k0 + tid; k < k1; k += kExactThreads) {
     const double4 v = src.load(b, k);
     const int first = __builtin_amdgcn_readfirstlane(lane);     // the wave's first active lane
 #pragma unroll 1
     for (int j = 0; j < kept; ++j) {
-      const unsigned long long m = __ballot(inlier_f64v(Eb + (size_t)mp[j] * kCandStride, v, kc));
+      const unsigned long long m = __ballot(inlier_f64v(&s_E[j][0], v, kc));
       if (lane == first && m) atomicAdd(&s_cnt[j], (int)__popcll(m));
     }
   }
   __syncthreads();
-  for (int c = tid; c < kept; c += 256)
+  for (int c = tid; c < kept; c += kExactThreads)
     if (s_cnt[c]) atomicAdd(cntT + (size_t)b * cmax + mp[c], s_cnt[c]);
+}
+
+// The one-sided pruning's second keep: of the candidates k_mf2_keep kept
+// (cmap_in, lead row 3), those whose upper count -- now over every point --
+// still reaches lb, compacted in order into cmap_out; lead rows 3 / 4 become
+// their count (row 4: 0 when k_mf2_exact takes them).  One block per pair.
+__global__ __launch_bounds__(1024) void k_mf2_keep_map(int cmax, const int32_t* __restrict__ cntT,
+                                                      int32_t* __restrict__ lead, const int32_t* __restrict__ cmap_in,
+                                                      int32_t* __restrict__ cmap_out, int exact_max) {
+  __shared__ int s_part[16];
+  __shared__ int s_base;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n = lead[3 * SFM_MAX_BATCH + b];
+  const long long lb = (long long)lead[0 * SFM_MAX_BATCH + b] + lead[2 * SFM_MAX_BATCH + b];
+  const int32_t* cnt = cntT + (size_t)b * cmax;
+  const int32_t* in = cmap_in + (size_t)b * cmax;
+  int32_t* out = cmap_out + (size_t)b * cmax;
+  if (tid == 0) s_base = 0;
+  __syncthreads();
+  for (int j0 = 0; j0 < n; j0 += 1024) {
+    const int j = j0 + tid;
+    const int c = j < n ? in[j] : 0;
+    const bool keep = j < n && (long long)cnt[c] >= lb;
+    const unsigned long long bal = __ballot(keep);
+    if (lane == 0) s_part[wv] = __popcll(bal);
+    __syncthreads();
+    int off = s_base + __popcll(bal & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wv; ++w) off += s_part[w];
+    if (keep) out[off] = c;
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int w = 0; w < 16; ++w) t += s_part[w];
+      s_base += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    lead[3 * SFM_MAX_BATCH + b] = s_base;
+    lead[4 * SFM_MAX_BATCH + b] = s_base > exact_max ? s_base : 0;
+  }
 }
 
 // After k_mf2_keep in the one-sided pruning: the kept candidates' (upper
