@@ -297,11 +297,16 @@ def score_roofline(use_mf, tflops, done, evals, skipped, cands, n, ms, traffic, 
             t = done * FLOP_PER_EVAL / (rocprof[0] * 1e-3) / 1e12
             rp = {"avg_launch_ms": round(rocprof[0], 4), "achieved": round(t, 3),
                   "frac": round(t / PEAK_F16_TFLOPS, 4), "source": rocprof[1],
-                  "note": "k_mf_cands + k_score_mf2 (+ k_mf2_split + k_mf2_lead + k_mf2_keep) per step from the committed rocprofv3 --stats "
+                  "note": "k_mf_cands + k_score_mf2 (+ k_mf2_split + k_mf2_lead + k_mf2_keep + k_mf2_keep_map + "
+                          "k_mf2_zero_kept + k_mf2_exact) per step from the committed rocprofv3 --stats "
                           "summary of this workload (a profiled run clocks lower than this one)"}
         pruned = scorer == "k_score_mf2+prune"
         kern = ("ransac_score (k_mf_cands + k_score_mf2 x3 + k_mf2_split + k_mf2_lead + k_mf2_keep: count-bound pruning)" if pruned
                 else "ransac_score (k_mf_cands + k_score_mf2)")
+        if pruned and upper is not None:
+            kern = ("ransac_score (k_mf_cands + k_score_mf2 one-sided x3 + k_mf2_split + k_mf2_lead + k_mf2_keep + "
+                    "k_mf2_keep_map + k_mf2_zero_kept + k_mf2_exact + k_score_mf2 two-sided: one-sided count-bound "
+                    "pruning)")
         return {"kernel": kern, "scorer": scorer, "bound": "mfma-f16", "achieved": round(tflops, 3),
                 "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s", "frac": round(tflops / PEAK_F16_TFLOPS, 4),
                 "mfma_issued": {"flop_per_eval": MF_MFMA_FLOP_PER_EVAL if upper is None else "96 one-sided, 128 two-sided",
@@ -629,7 +634,8 @@ def _main_gpu(args, dist):
                                        traffic.get("ransac_score"), traffic_src,
                                        rocprof_kernel_ms(args, ("k_mf_cands", "k_score_mf2"),
                                                          optional=("k_mf2_split", "k_mf2_lead", "k_mf2_keep",
-                                                                   "k_mf2_zero_kept")),
+                                                                   "k_mf2_keep_map", "k_mf2_zero_kept",
+                                                                   "k_mf2_exact")),
                                        _lib.last_scorer(), upper_work),
             "roofline_sweep": {"kernel": "plane_sweep", "bound": "hbm", "achieved": round(sweep_gbs, 1),
                                "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(sweep_gbs / PEAK_HBM_GBS, 4),

@@ -7,7 +7,7 @@
 # the first failure.  SKIP_TESTS / SKIP_PROF / SKIP_PMC / SKIP_CONFIGS=1 skip
 # a part.  scripts/collect_evidence.py copies the results into profiles/.
 set -u
-R=${R:-r05}
+R=${R:-r06}
 mkdir -p gpurun_out
 export PYTHONDONTWRITEBYTECODE=1
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
