@@ -1035,8 +1035,14 @@ __device__ __forceinline__ void sweep_tile_fast(const float* __restrict__ ref, c
   }
 }
 
+// bf16 volumes at NJ = 2 (the default; round 6): 8 waves per SIMD instead of the 6 the allocator
+// picks (76 -> 64 VGPRs, a 48-byte spill outside the fast path): the tap
+// gathers' latency is what the extra waves hide -- the C3 sweep 0.363-0.368
+// -> 0.351-0.355 ms in three alternating rounds on one box
+// (profiles/r06_sweep_occupancy_ab.txt); fp32 kernels already run at 8.
 template <typename OutT, int NQ, int NJ>
-__global__ __launch_bounds__(kSwThreads) void k_sweep_tile(const float* __restrict__ ref,
+__global__ __launch_bounds__(kSwThreads) __attribute__((amdgpu_waves_per_eu(sizeof(OutT) == 2 && NJ == 2 ? 8 : 1)))
+void k_sweep_tile(const float* __restrict__ ref,
                                                            const f32x4* __restrict__ tq,
                                                            const float* __restrict__ pose,
                                                            const float* __restrict__ K4,
