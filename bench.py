@@ -81,7 +81,11 @@ def parse(argv=None):
     ap.add_argument("--no-regularize", action="store_true",
                     help="skip the (unscored) PSNet 3-D regularisation roofline line after the timed region")
     ap.add_argument("--fused", action="store_true",
-                    help="RANSAC reads the flow directly (sfm_ransac5_flow) instead of materialised correspondences")
+                    help="(the default for dense flow since round 6) RANSAC reads the flow directly "
+                         "(sfm_ransac5_flow, SURVEY 8f row 2) instead of materialised correspondences")
+    ap.add_argument("--no-fused", action="store_true",
+                    help="materialise the correspondences first (sfm_flow_to_points + sfm_ransac5_packed): "
+                         "0.6 - 1.5 %% slower at c2, profiles/r06_fused_ab.txt")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads for the CPU baseline: 16 = the host-core share one GPU gets on the "
                          "MI355X pool (nproc there reports the whole 256-thread host)")
@@ -532,7 +536,8 @@ def _main_gpu(args, dist):
         k, v = kv.split("=")
         _lib.tune(k.strip(), int(v))
     hp = TwoViewHotPath(B, hw, fhw, C, args.nlabel, args.iters, args.threshold, 1.0, rescale_depth=True,
-                        norm_target=0.6, cost_dtype=cost_dtype, device=dev, fused=args.fused,
+                        norm_target=0.6, cost_dtype=cost_dtype, device=dev,
+                        fused=not args.keypoints and not args.no_fused,
                         keypoints=None if kp is None else (kp, [args.keypoints] * B),
                         overlap_ref=False if args.overlap_ref == "0" else args.overlap_ref,
                         gate_scorer=not args.no_gate)
@@ -601,7 +606,8 @@ def _main_gpu(args, dist):
     traffic, traffic_src = pmc_traffic(args)
     if rank == 0:
         pairs = world * B * args.steps
-        corr = (f"{args.keypoints} SIFT-like keypoints" if args.keypoints else f"dense flow (N={hp.n})")
+        corr = (f"{args.keypoints} SIFT-like keypoints" if args.keypoints
+                else f"dense flow (N={hp.n}{', read by the RANSAC kernels' if hp.fused else ''})")
         out = {
             "metric": metric_name(args.nlabel, hwtxt),
             "value": round(pairs / elapsed, 3),

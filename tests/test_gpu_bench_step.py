@@ -1,7 +1,7 @@
 """The bench's own step against the oracle: TwoViewHotPath.step at the C2
 shape (KITTI 376x1242 dense flow, N = 435,032, H = 4096, nlabel = 128, fp32
-volume), two pairs, through the default dispatch (k_score_mf2 with
-count-bound pruning, asserted).  Winner, inlier count, E and P of every pair
+volume), two pairs, through the default dispatch (dense flow read by the
+RANSAC kernels, k_score_mf2 with count-bound pruning, asserted).  Winner, inlier count, E and P of every pair
 equal the oracle's on the step's own correspondences (reference:
 kernel_functions.cu:141-264, essential_matrix.cu:190-280), and the step's
 cost volume (sfm_plane_sweep_psnet: quarter intrinsics and RESCALE_DEPTH
@@ -26,8 +26,9 @@ def test_bench_step_c2_shape_vs_oracle(cuda):
     fhw = synth.feature_hw(hw)
     flow, K, _, _ = synth.kitti_pair_batch(B, seed=1000, hw=hw, device=cuda)
     ref_fea, tgt_fea = synth.features(B, C, fhw[0], fhw[1], seed=0, device=cuda)
+    # the bench's configuration: dense flow read by the RANSAC kernels (fused)
     hp = TwoViewHotPath(B, hw, fhw, C, L, iters, thr, 1.0, rescale_depth=True, norm_target=0.6,
-                        cost_dtype=torch.float32, device=cuda)
+                        cost_dtype=torch.float32, device=cuda, fused=True)
     assert hp.n == 435032
     E, P, inl, cost = hp.step(flow, K, ref_fea, tgt_fea)
     torch.cuda.synchronize()
@@ -47,8 +48,12 @@ def test_bench_step_c2_shape_vs_oracle(cuda):
     assert float(err.max()) <= 0.0, float((got[:, C:] - want[:, C:]).abs().max())
     assert float(want[:, C:].abs().sum()) > 0.0       # the step's poses project into the image
     _, _, _, win = hp.pose(flow, K)                        # the same call again: the winners
+    # the step's correspondences as the fused kernels read them (bit-identical
+    # to the materialised ones: test_gpu_ransac.py::test_fused_flow_path_equals_packed)
+    from sfm_amd import ransac
+    pts = ransac.flow_to_points(flow, Kinv)
     for b in range(B):
-        p = hp.pts[b].cpu().numpy()
+        p = pts[b].cpu().numpy()
         ref = R.ransac5(np.ascontiguousarray(p[:, :2]), np.ascontiguousarray(p[:, 2:]), iters=iters, thr=thr,
                         nthreads=16)
         assert int(win[b]) == ref["winner"] and int(inl[b]) == ref["inliers"], (b, int(inl[b]), ref["inliers"])
