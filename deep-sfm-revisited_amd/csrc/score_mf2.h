@@ -651,7 +651,13 @@ __global__ __launch_bounds__(1024) void k_mf2_lead(const Src src, PairParams pp,
     const int k1 = (int)((long long)M * (blockIdx.x + 1) / gridDim.x);
     const double* El = candE + ((size_t)b * cmax + ldr) * kCandStride;
     int r = 0;
-    for (int k = k0 + tid; k < k1; k += blockDim.x) r += inlier_f64v(El, src.load(b, k), kc) ? 1 : 0;
+    const int T = (int)blockDim.x;
+    for (int k = k0 + tid; k < k1; k += 2 * T) {             // two independent chains per pass
+      const bool ob = k + T < k1;
+      const double4 va = src.load(b, k), vb = src.load(b, ob ? k + T : k);
+      r += inlier_f64v(El, va, kc) ? 1 : 0;
+      r += (ob && inlier_f64v(El, vb, kc)) ? 1 : 0;
+    }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) r += __shfl_xor(r, d, 64);
     if (lane == 0) s_part[wv] = r;
@@ -784,13 +790,18 @@ __global__ __launch_bounds__(kExactThreads) void k_mf2_exact(const Src src, Pair
   const int k0 = (int)((long long)M * blockIdx.x / gridDim.x);
   const int k1 = (int)((long long)M * (blockIdx.x + 1) / gridDim.x);
   const int lane = tid & 63;
-  for (int k = k0 + tid; k < k1; k += kExactThreads) {
-    const double4 v = src.load(b, k);
-    const int first = __builtin_amdgcn_readfirstlane(lane);     // the wave's first active lane
+  // two points per thread and pass (two independent float64 chains in
+  // flight); the block's loop is uniform, so every lane takes part in the
+  // ballots and lane 0 publishes
+  for (int base = k0; base < k1; base += 2 * kExactThreads) {
+    const int ka = base + tid, kb = base + kExactThreads + tid;
+    const bool oa = ka < k1, ob = kb < k1;
+    const double4 va = src.load(b, oa ? ka : k0), vb = src.load(b, ob ? kb : k0);
 #pragma unroll 1
     for (int j = 0; j < kept; ++j) {
-      const unsigned long long m = __ballot(inlier_f64v(&s_E[j][0], v, kc));
-      if (lane == first && m) atomicAdd(&s_cnt[j], (int)__popcll(m));
+      const bool ia = inlier_f64v(&s_E[j][0], va, kc), ib = inlier_f64v(&s_E[j][0], vb, kc);
+      const int n = (int)__popcll(__ballot(oa && ia)) + (int)__popcll(__ballot(ob && ib));
+      if (lane == 0 && n) atomicAdd(&s_cnt[j], n);
     }
   }
   __syncthreads();
