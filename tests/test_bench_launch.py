@@ -244,3 +244,20 @@ def test_pmc_summary_sums_template_instances(tmp_path):
     k = json.load(open(dst))["kernels"]["ransac_score"]
     assert k["launches_sampled"] == {"k_mf_cands": 2, "k_score_mf2": 6}
     assert abs(k["SQ_WAVES"] - 116.0) < 1e-9               # 10 + 100 + 1 + 5 per step
+
+
+def test_one_sided_pruning_work_accounting():
+    """The scorer's roofline line under the one-sided pruning (round 6): the
+    algorithmic work stays (candidates x N - skipped) x 50 FLOP, the MFMA pipe
+    use counts 96 FLOP per one-sided and 128 per two-sided evaluation, and the
+    work string names both passes."""
+    sys.path.insert(0, ROOT)
+    import bench
+    done, evals, skipped = 3000, 3200, 200
+    r0 = bench.score_roofline(True, 1.0, done, evals, skipped, 10, 320, 2.0, None, None, scorer="k_score_mf2+prune")
+    r1 = bench.score_roofline(True, 1.0, done, evals, skipped, 10, 320, 2.0, None, None, scorer="k_score_mf2+prune",
+                              upper=(done, 2 * 320, 2))
+    assert r0["mfma_issued"]["tflops"] == round(done * 128 / 2e-3 / 1e12, 1)
+    assert r1["mfma_issued"]["tflops"] == round((done * 96 + 2 * 320 * 128) / 2e-3 / 1e12, 1)
+    assert "one-sided pass" in r1["work"] and "2 of 10 candidates kept" in r1["work"]
+    assert "one-sided" in r1["kernel"] and "one-sided" not in r0["kernel"]
