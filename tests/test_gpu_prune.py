@@ -210,3 +210,36 @@ def test_mf2_one_sided_exact_count_paths(cuda, exact_max):
         assert torch.equal(x, y)
     kept = ransac.kept_candidates(ws, 2, 4)
     assert int(kept.min()) >= 1 and int(kept.sum()) < 0.1 * sum(ransac.candidate_counts(ws, 2, 4))
+
+
+@pytest.mark.parametrize("exact_max", [256, 0])
+@pytest.mark.parametrize("noise_px,outlier_frac", [(0.0, 0.0), (0.0, 0.5), (0.5, 1.0)])
+def test_mf2_pruning_ties_and_extremes(cuda, noise_px, outlier_frac, exact_max):
+    """Noise-free pairs: many hypotheses count every point (or every true
+    inlier) and tie at the top, so the one-sided pass must keep all of them
+    and the winner is decided by the first-max rule alone (hundreds kept:
+    past score_mf_exact_max, the two-sided matrix-core count through the
+    index map).  All-outlier pairs: every count small, the pruning point near
+    the end.  Pruned (both forms) == unpruned in every case."""
+    from sfm_amd import _lib, ransac, synth
+    flow, K, _, _ = synth.kitti_pair_batch(2, seed=9, hw=(200, 320), noise_px=noise_px,
+                                           outlier_frac=outlier_frac, device=cuda)
+    pts = ransac.flow_to_points(flow, torch.inverse(K))
+    N = pts.shape[1]
+    ref = ransac.ransac5_batched(pts, None, None, None, 2, 1e-4, return_scores=True)
+    _lib.tune("score_mf_exact_max", exact_max)
+    out, kernels = _both(pts, iters=2)
+    assert kernels[1] == "k_score_mf2+prune" and kernels[2] == "k_score_mf2+prune"
+    _same(out)
+    for x, y in zip(out[1][:4], ref[:4]):
+        assert torch.equal(x, y.cpu())
+    inl, scores = ref[2].cpu(), ref[4].cpu()
+    ties = (scores == inl[:, None]).sum(dim=1)
+    if outlier_frac == 0.0:                       # the regime: (nearly) every point an inlier, many-way ties
+        assert int(inl.min()) > 0.99 * N and int(ties.min()) > 10
+    elif outlier_frac == 0.5:
+        assert 0.4 * N < int(inl.min()) and int(inl.max()) < 0.7 * N
+    else:
+        assert int(inl.max()) < 0.5 * N
+    if outlier_frac < 1.0:
+        assert int(out[1][5]) >= int(ties.sum())  # every tied hypothesis' candidate was kept
