@@ -261,3 +261,17 @@ def test_one_sided_pruning_work_accounting():
     assert r1["mfma_issued"]["tflops"] == round((done * 96 + 2 * 320 * 128) / 2e-3 / 1e12, 1)
     assert "one-sided pass" in r1["work"] and "2 of 10 candidates kept" in r1["work"]
     assert "one-sided" in r1["kernel"] and "one-sided" not in r0["kernel"]
+
+
+def test_clock_probe_edits_apply_to_the_sources():
+    """scripts/build_clock_probe.py patches a temporary copy of score_mf2.h at
+    fixed anchors: each must still occur exactly once in the current source,
+    or the diagnostic behind profiles/r06_scorer_clock.txt no longer builds."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("build_clock_probe",
+                                                  os.path.join(ROOT, "scripts", "build_clock_probe.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    src = open(os.path.join(ROOT, "deep-sfm-revisited_amd", "csrc", "score_mf2.h")).read()
+    for old, _ in mod.EDITS:
+        assert src.count(old) == 1, old
